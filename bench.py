@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""Device-resident RS/XOR encode+rebuild throughput on MI355X.
+
+Step (N=1, BASELINE.json configs[2] + configs[3]): one redundancy set of
+p = 11 members, RS(8+3) (redset ranks=11, encoding=3), 64 MiB chunks, all
+cells resident in HBM: encode the parity of all 11 stripes, then rebuild
+members {1, 2} from the survivors. Both passes run the gf_mac HIP kernel.
+`value` = algorithmic bytes of both passes / wall time of the step, GB/s
+(10^9 B). Algorithmic bytes per stripe: encode (d + e)*C, rebuild (d + m)*C
+(SURVEY.md §8d).
+
+N>1 (torchrun, one process per GPU, RCCL): weak scaling -- every GPU hosts 11
+members; the world holds N sets whose members are spread round-robin over the
+GPUs, and every stripe is computed column-sharded over all GPUs after an
+all-to-all gather of cell slices (redset_amd.dist); the exchange is inside the
+timed step.
+
+Prints ONE JSON line on rank 0.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
+MIB = 1 << 20
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--ranks", type=int, default=11, help="redset set size p")
+    ap.add_argument("--encoding", type=int, default=3, help="parity cells per stripe e")
+    ap.add_argument("--chunk-mib", type=float, default=64.0)
+    ap.add_argument("--lost", default="1,2", help="members rebuilt each step")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port beside (rank 0, N=1)")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
+    return ap.parse_args()
+
+
+def cpu_baseline(p, e, lost, target_s):
+    """Reference CPU path on host cores: redset_reedsolomon_encode_pthreads
+    (src/redset_reedsolomon_pthreads.c:567-699) for the encode and the serial
+    CPU decode the reference falls back to for PTHREADS (src/redset_reedsolomon.c:
+    994-1000), both as restated in oracle/ (kind "port"), on a bounded sample:
+    the same set shape with a smaller chunk."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import oracle_lib
+
+    oracle_lib.build()
+    st = oracle_lib.OracleRS(p, e)
+    d = p - e
+    chunk = 4 * MIB
+    lofi, parity = oracle_lib.random_set(p, d, e, chunk, seed=7)
+    passes, t_enc, t_reb, threads = 0, 0.0, 0.0, 0
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        threads = st.encode_pthreads(lofi, parity, chunk, slice_bytes=MIB)
+        t1 = time.perf_counter()
+        lf = [x if r not in lost else np.zeros_like(x) for r, x in enumerate(lofi)]
+        pr = [x.copy() if r not in lost else np.zeros_like(x) for r, x in enumerate(parity)]
+        st.rebuild_set(lost, lf, pr, chunk, slice_bytes=MIB)
+        t2 = time.perf_counter()
+        t_enc += t1 - t0
+        t_reb += t2 - t1
+        passes += 1
+        if time.perf_counter() - t_start >= target_s:
+            break
+    enc_bytes = p * (d + e) * chunk * passes
+    reb_bytes = p * (d + len(lost)) * chunk * passes
+    return {
+        "value": round((enc_bytes + reb_bytes) / (t_enc + t_reb) / 1e9, 4),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (
+            f"{passes} x (RS({d}+{e}) full-set encode with {threads} pthreads + serial rebuild of "
+            f"members {lost}), p={p}, chunk={chunk // MIB} MiB (host buffers); encode "
+            f"{enc_bytes / t_enc / 1e9:.3f} GB/s, rebuild {reb_bytes / t_reb / 1e9:.3f} GB/s"
+        ),
+        "encode_GBps": round(enc_bytes / t_enc / 1e9, 4),
+        "rebuild_GBps": round(reb_bytes / t_reb / 1e9, 4),
+        "host_cpus": os.cpu_count(),
+    }
+
+
+def load_traffic(path, kernel_prefix):
+    """HBM bytes per launch of the dominant kernel from a rocprofv3 PMC pass
+    (tools/pmc_traffic.py writes this file); None if absent."""
+    try:
+        with open(path) as f:
+            t = json.load(f)
+        return t.get(kernel_prefix)
+    except (OSError, ValueError):
+        return None
+
+
+def main():
+    args = parse()
+    import torch
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        if world == 1 and args.gpus > 1:
+            print(json.dumps({"error": f"--gpus {args.gpus} needs torchrun with {args.gpus} processes"}))
+            sys.exit(2)
+    torch.cuda.set_device(local_rank)
+    dist_on = world > 1
+    if dist_on:
+        import torch.distributed as dist
+
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+
+    import redset_amd
+
+    redset_amd.load()
+    p, e = args.ranks, args.encoding
+    d = p - e
+    chunk = int(args.chunk_mib * MIB)
+    lost = sorted(int(x) for x in args.lost.split(",") if x != "")
+    stream = torch.cuda.current_stream()
+
+    if dist_on:
+        from redset_amd import dist as rdist
+
+        runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank)
+        step = runner.step
+        bytes_per_step = runner.algorithmic_bytes * world
+        enc_plan = runner.local_encode_plan
+        reb_plan = runner.local_rebuild_plan
+    else:
+        codec = redset_amd.RSCodec(p, e)
+        lay = redset_amd.SetLayout.allocate(p, d, e, chunk)
+        g = torch.Generator(device="cuda")
+        g.manual_seed(1234)
+        for r in range(p):
+            n = lay.lofi(r).numel()
+            lay.lofi(r).copy_(torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g))
+        enc_plan = codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+        reb_plan = codec.plan_rebuild(lost, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+        bytes_per_step = (enc_plan.bytes_read + enc_plan.bytes_written
+                          + reb_plan.bytes_read + reb_plan.bytes_written)
+        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
+        cur = {"i": -1}
+
+        def step():
+            i = cur["i"]
+            if i >= 0:
+                ev[i][0].record(stream)
+            enc_plan.execute(stream)
+            if i >= 0:
+                ev[i][1].record(stream)
+            reb_plan.execute(stream)
+            if i >= 0:
+                ev[i][2].record(stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        if not dist_on:
+            cur["i"] = k
+        step()
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = bytes_per_step / (elapsed / args.steps) / 1e9
+
+    result = {
+        "metric": "GB/s device-resident RS/XOR encode+rebuild vs HBM peak, 1/2/4/8 MI355X",
+        "value": round(value, 2),
+        "unit": "GB/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms_per_step, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "u8",
+        "data": "synthetic: uniform random bytes (torch.randint on device), all cells resident in HBM",
+        "config": {
+            "workload": (f"RS({d}+{e}) p={p} e={e}, chunk {args.chunk_mib:g} MiB: full-set encode of all "
+                         f"{p} stripes + rebuild of members {lost}"),
+            "ranks": p,
+            "encoding": e,
+            "chunk_bytes": chunk,
+            "sets": world,
+            "bytes_per_step": bytes_per_step,
+            "parallelism": "single GPU" if world == 1 else f"column-sharded over {world} GPUs, RCCL all-to-all",
+        },
+    }
+    if not dist_on:
+        enc_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
+        reb_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
+        eb = enc_plan.bytes_read + enc_plan.bytes_written
+        rb = reb_plan.bytes_read + reb_plan.bytes_written
+        achieved = (eb + rb) / ((enc_ms + reb_ms) * 1e-3) / 1e9
+        traffic = load_traffic(args.traffic_json, "gf_mac_kernel<8>")
+        result["roofline"] = {
+            "bound": "hbm",
+            "kernel": "gf_mac_kernel<8> (redset_amd/csrc/codec_kernels.hip)",
+            "achieved": round(achieved, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4),
+            "traffic": traffic,
+            "algorithmic_bytes_per_launch": {"encode": eb, "rebuild": rb},
+            "avg_launch_ms": {"encode": round(enc_ms, 4), "rebuild": round(reb_ms, 4)},
+        }
+        result["breakdown"] = {
+            "encode_GBps": round(eb / (enc_ms * 1e-3) / 1e9, 1),
+            "encode_read_GBps": round(enc_plan.bytes_read / (enc_ms * 1e-3) / 1e9, 1),
+            "rebuild_GBps": round(rb / (reb_ms * 1e-3) / 1e9, 1),
+        }
+        if args.cpu_baseline and rank == 0:
+            result["cpu_baseline"] = cpu_baseline(p, e, lost, args.cpu_seconds)
+    else:
+        result.update(runner.report(elapsed / args.steps))
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if dist_on:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

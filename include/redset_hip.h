@@ -1,0 +1,147 @@
+/*
+ * redset_hip.h -- C ABI of the MI355X (gfx950) Reed-Solomon / XOR codec that
+ * replaces redset's encode/decode backends.
+ *
+ * Everything here is plain C: integers, sizes and pointers. Buffers named
+ * "device" are HIP device pointers; `stream` is a hipStream_t passed as
+ * void* (NULL = the default stream). Return codes follow redset:
+ * REDSET_SUCCESS (0, src/redset.h:24) or REDSET_FAILURE (1,
+ * src/redset_util.h:19); HIP errors map to REDSET_FAILURE and
+ * redset_hip_last_error() says why.
+ *
+ * Where the reference dispatches to a backend (src/redset_reedsolomon.c:
+ * 522-545, :986-1006; src/redset_xor.c:399-420, :650-671), a maintainer adds
+ * a REDSET_ENCODE_HIP case that calls these functions; INTEGRATION.md shows
+ * that glue.
+ *
+ * Data layout in HBM ("set layout"): member r of a redundancy set of p
+ * members owns a logical-file region lofi[r] holding its data cells
+ * (p-e for RS, p-1 for XOR) and a redundancy region parity[r] holding its
+ * e parity cells (1 for XOR). Cell s of either region starts at
+ * base + s * cell_stride, cell_stride >= chunk_size. This mirrors the
+ * reference's logical file (segment s at s*chunk_size, src/redset_
+ * reedsolomon.c:334-335) and redundancy file (slot i at header + i*chunk_size,
+ * :380-381) with an optional pad so every cell can start 16-B aligned.
+ * Cells at a 16-B aligned address take the vector path; others work, slowly.
+ */
+#ifndef REDSET_HIP_H
+#define REDSET_HIP_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#ifndef REDSET_SUCCESS
+#define REDSET_SUCCESS (0)
+#endif
+#ifndef REDSET_FAILURE
+#define REDSET_FAILURE (1)
+#endif
+
+typedef struct redset_hip_rs redset_hip_rs;      /* GF tables + encoding matrix */
+typedef struct redset_hip_plan redset_hip_plan;  /* prepared kernel launches */
+
+enum {
+  REDSET_HIP_PLAN_RS_ENCODE = 1,
+  REDSET_HIP_PLAN_RS_REBUILD = 2,
+  REDSET_HIP_PLAN_XOR_ENCODE = 3,
+  REDSET_HIP_PLAN_XOR_REBUILD = 4
+};
+
+typedef struct {
+  int kind;                          /* REDSET_HIP_PLAN_* */
+  int ranks;                         /* p */
+  int encoding;                      /* e (1 for XOR) */
+  int missing;                       /* erased members (rebuild plans) */
+  int launches;                      /* kernel launches per execute */
+  int jobs;                          /* stripe jobs over all launches */
+  size_t chunk_size;                 /* bytes per cell */
+  unsigned long long bytes_read;     /* algorithmic bytes read per execute */
+  unsigned long long bytes_written;  /* algorithmic bytes written per execute */
+} redset_hip_plan_info;
+
+/* ---- field, matrix, layout ------------------------------------------- */
+
+/* Build GF(2^8) tables and the (p+e) x p encoding matrix.
+ * Replaces redset_rs_gf_alloc (src/redset_reedsolomon_common.c:727-757) as
+ * called from redset_construct_rs (src/redset_reedsolomon.c:169-185); same
+ * validity rule: 1 <= encoding < ranks, ranks + encoding <= 256. */
+int redset_hip_rs_create(int ranks, int encoding, redset_hip_rs** out);
+/* Replaces redset_rs_gf_delete (src/redset_reedsolomon_common.c:759-769). */
+void redset_hip_rs_destroy(redset_hip_rs* rs);
+/* Copies the (p+e) x p matrix (state->mat, src/redset_internal.h:88) as bytes. */
+int redset_hip_rs_matrix(const redset_hip_rs* rs, unsigned char* mat_out);
+/* Same results as redset_rs_get_encoding_id / redset_rs_get_data_id
+ * (src/redset_reedsolomon_common.c:822-853). */
+int redset_hip_rs_get_encoding_id(int ranks, int encoding, int rank, int chunk_id);
+int redset_hip_rs_get_data_id(int ranks, int encoding, int rank, int chunk_id);
+
+/* ---- whole-set plans (all members' cells resident on one device) ----- */
+
+/* Parity of every stripe of the set: the work redset_reedsolomon_encode
+ * (src/redset_reedsolomon.c:280-402) does across all p ranks; member r's
+ * parity slot i = stripe (r+i) mod p, row p+i. lofi/parity: p device pointers. */
+int redset_hip_rs_plan_encode(const redset_hip_rs* rs, unsigned char* const* lofi,
+                              unsigned char* const* parity, size_t chunk_size,
+                              size_t cell_stride, redset_hip_plan** out);
+
+/* Rebuild the cells of `missing` erased members (ascending, as
+ * redset_recover_rs builds them, src/redset_reedsolomon.c:1111-1119) in every
+ * stripe; replaces redset_reedsolomon_decode (src/redset_reedsolomon.c:
+ * 570-785) / redset_recover_rs_rebuild_serial (src/redset_reedsolomon_
+ * serial.c:165-343). Outputs land in the erased members' lofi/parity cells.
+ * Fails if missing > encoding (src/redset_reedsolomon.c:1096). */
+int redset_hip_rs_plan_rebuild(const redset_hip_rs* rs, int missing, const int* rebuild_ranks,
+                               unsigned char* const* lofi, unsigned char* const* parity,
+                               size_t chunk_size, size_t cell_stride, redset_hip_plan** out);
+
+/* XOR parity of every stripe: member r's cell = XOR of every other member's
+ * cell of stripe r (src/redset_xor.c:220-295). xorc: p device pointers. */
+int redset_hip_xor_plan_encode(int ranks, unsigned char* const* lofi, unsigned char* const* xorc,
+                               size_t chunk_size, size_t cell_stride, redset_hip_plan** out);
+
+/* Rebuild member `root` (src/redset_xor.c:441-531,
+ * src/redset_xor_serial.c:161-275). */
+int redset_hip_xor_plan_rebuild(int ranks, int root, unsigned char* const* lofi,
+                                unsigned char* const* xorc, size_t chunk_size, size_t cell_stride,
+                                redset_hip_plan** out);
+
+/* Enqueue the plan's kernels on `stream`; no host synchronisation, no
+ * allocation (safe inside hipStreamBeginCapture). */
+int redset_hip_plan_execute(const redset_hip_plan* plan, void* stream);
+int redset_hip_plan_get_info(const redset_hip_plan* plan, redset_hip_plan_info* info);
+void redset_hip_plan_destroy(redset_hip_plan* plan);
+
+/* ---- stripe primitives (one stripe, device pointers) ----------------- */
+
+/* out[j] = (out[j] ^) sum_i coeffs[j*nin + i] * in[i] over GF(2^8), for
+ * nbytes bytes; nin <= 16, nout <= 4 per call. One pass replaces nout*nin
+ * calls of redset_rs_reduce_buffer_multadd (src/redset_reedsolomon_common.c:
+ * 786-819) and, with a decode matrix, redset_rs_reduce_decode +
+ * redset_rs_gaussian_solve (:855-899, :570-630). */
+int redset_hip_gf_combine(const unsigned char* const* in, int nin, unsigned char* const* out,
+                          int nout, const unsigned char* coeffs, size_t nbytes, int accumulate,
+                          void* stream);
+
+/* out = (out ^) XOR of nin inputs, nin <= 16 (reduce_xor, src/redset_xor.c:35-42). */
+int redset_hip_xor_combine(const unsigned char* const* in, int nin, unsigned char* out,
+                           size_t nbytes, int accumulate, void* stream);
+
+/* Host-side decode matrix for one stripe: rows = missing outputs, columns =
+ * the p members (0 for erased members / unused cells). coef_out: missing x p
+ * bytes. Equals the reference's reduce_decode + gaussian_solve as one linear
+ * map. */
+int redset_hip_rs_decode_matrix(const redset_hip_rs* rs, int missing, const int* rebuild_ranks,
+                                int chunk_id, unsigned char* coef_out);
+
+/* Text of the last failure on this thread ("" if none). */
+const char* redset_hip_last_error(void);
+/* Library version string. */
+const char* redset_hip_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* REDSET_HIP_H */

@@ -1,0 +1,136 @@
+"""ctypes binding of the in-tree HIP codec library (redset_amd/lib/libredset_hip.so).
+
+The library is the product: every codec call below goes through it. There is
+no CPU fallback -- if the shared object is missing or fails to load, importing
+:mod:`redset_amd` still works (so CPU-only tooling can inspect the package),
+but the first call raises :class:`RedsetHipUnavailable` loudly.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from ctypes import POINTER, c_char_p, c_int, c_size_t, c_ubyte, c_ulonglong, c_void_p
+
+LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libredset_hip.so")
+
+REDSET_SUCCESS = 0
+REDSET_FAILURE = 1
+
+PLAN_RS_ENCODE = 1
+PLAN_RS_REBUILD = 2
+PLAN_XOR_ENCODE = 3
+PLAN_XOR_REBUILD = 4
+
+# every symbol include/redset_hip.h declares (checked by tests/test_abi.py)
+EXPORTED_SYMBOLS = (
+    "redset_hip_rs_create",
+    "redset_hip_rs_destroy",
+    "redset_hip_rs_matrix",
+    "redset_hip_rs_get_encoding_id",
+    "redset_hip_rs_get_data_id",
+    "redset_hip_rs_plan_encode",
+    "redset_hip_rs_plan_rebuild",
+    "redset_hip_xor_plan_encode",
+    "redset_hip_xor_plan_rebuild",
+    "redset_hip_plan_execute",
+    "redset_hip_plan_get_info",
+    "redset_hip_plan_destroy",
+    "redset_hip_gf_combine",
+    "redset_hip_xor_combine",
+    "redset_hip_rs_decode_matrix",
+    "redset_hip_last_error",
+    "redset_hip_version",
+)
+
+
+class RedsetHipUnavailable(RuntimeError):
+    """The HIP codec library could not be loaded."""
+
+
+class RedsetHipError(RuntimeError):
+    """A codec call returned REDSET_FAILURE."""
+
+
+class PlanInfo(ctypes.Structure):
+    _fields_ = [
+        ("kind", c_int),
+        ("ranks", c_int),
+        ("encoding", c_int),
+        ("missing", c_int),
+        ("launches", c_int),
+        ("jobs", c_int),
+        ("chunk_size", c_size_t),
+        ("bytes_read", c_ulonglong),
+        ("bytes_written", c_ulonglong),
+    ]
+
+
+_PP = POINTER(c_void_p)
+
+_SIGNATURES = {
+    "redset_hip_rs_create": (c_int, [c_int, c_int, POINTER(c_void_p)]),
+    "redset_hip_rs_destroy": (None, [c_void_p]),
+    "redset_hip_rs_matrix": (c_int, [c_void_p, POINTER(c_ubyte)]),
+    "redset_hip_rs_get_encoding_id": (c_int, [c_int, c_int, c_int, c_int]),
+    "redset_hip_rs_get_data_id": (c_int, [c_int, c_int, c_int, c_int]),
+    "redset_hip_rs_plan_encode": (c_int, [c_void_p, _PP, _PP, c_size_t, c_size_t, POINTER(c_void_p)]),
+    "redset_hip_rs_plan_rebuild": (
+        c_int,
+        [c_void_p, c_int, POINTER(c_int), _PP, _PP, c_size_t, c_size_t, POINTER(c_void_p)],
+    ),
+    "redset_hip_xor_plan_encode": (c_int, [c_int, _PP, _PP, c_size_t, c_size_t, POINTER(c_void_p)]),
+    "redset_hip_xor_plan_rebuild": (c_int, [c_int, c_int, _PP, _PP, c_size_t, c_size_t, POINTER(c_void_p)]),
+    "redset_hip_plan_execute": (c_int, [c_void_p, c_void_p]),
+    "redset_hip_plan_get_info": (c_int, [c_void_p, POINTER(PlanInfo)]),
+    "redset_hip_plan_destroy": (None, [c_void_p]),
+    "redset_hip_gf_combine": (c_int, [_PP, c_int, _PP, c_int, POINTER(c_ubyte), c_size_t, c_int, c_void_p]),
+    "redset_hip_xor_combine": (c_int, [_PP, c_int, c_void_p, c_size_t, c_int, c_void_p]),
+    "redset_hip_rs_decode_matrix": (c_int, [c_void_p, c_int, POINTER(c_int), c_int, POINTER(c_ubyte)]),
+    "redset_hip_last_error": (c_char_p, []),
+    "redset_hip_version": (c_char_p, []),
+}
+
+_lib = None
+
+
+def load(path: str = LIB_PATH) -> ctypes.CDLL:
+    """Load (once) and return the codec library; raise if it is unavailable."""
+    global _lib
+    if _lib is not None and path == LIB_PATH:
+        return _lib
+    lib = open_library(path)
+    if path == LIB_PATH:
+        _lib = lib
+    return lib
+
+
+def open_library(path: str) -> ctypes.CDLL:
+    """Open the library at ``path`` and bind its signatures (no caching)."""
+    if not os.path.exists(path):
+        raise RedsetHipUnavailable(
+            f"HIP codec library not built: {path} is missing "
+            "(run `python -c 'import __graft_entry__ as g; g.build()'` or `make -C redset_amd/csrc`)"
+        )
+    try:
+        lib = ctypes.CDLL(path)
+    except OSError as exc:  # pragma: no cover - depends on the box
+        raise RedsetHipUnavailable(f"cannot load {path}: {exc}") from exc
+    for name, (res, args) in _SIGNATURES.items():
+        fn = getattr(lib, name)
+        fn.restype = res
+        fn.argtypes = args
+    return lib
+
+
+def check(rc: int, what: str) -> None:
+    if rc != REDSET_SUCCESS:
+        msg = load().redset_hip_last_error().decode(errors="replace")
+        raise RedsetHipError(f"{what} failed: {msg}")
+
+
+def ptr_array(ptrs) -> ctypes.Array:
+    """Host array of device pointers (ints) for the C ABI."""
+    arr = (c_void_p * len(ptrs))()
+    for i, p in enumerate(ptrs):
+        arr[i] = int(p)
+    return arr

@@ -1,0 +1,66 @@
+// codec_kernels.h -- device-side job descriptors shared by the kernels
+// (codec_kernels.hip) and the host planner (redset_hip.cpp).
+#pragma once
+
+#include <cstddef>
+#include <cstdint>
+
+namespace redset_hip {
+
+// Most inputs one kernel pass combines, and most outputs it produces.
+// An output's 4 partial products are packed into one LDS dword per table
+// entry, so 4 outputs cost the same lookups as 1. Wider stripes or more
+// erasures are split into passes by the planner.
+constexpr int kMaxIn = 16;
+constexpr int kMaxOut = 4;
+
+// One stripe (or one pass over a slice of a stripe's members):
+// out[j] (^)= sum_i coef[j][i] * in[i] over GF(2^8), byte by byte.
+struct GfJob {
+  const uint8_t* in[kMaxIn];
+  uint8_t* out[kMaxOut];
+  uint8_t coef[kMaxOut][kMaxIn];
+};
+
+// One launch of the GF multiply-accumulate kernel over `njobs` jobs.
+struct GfLaunch {
+  const GfJob* jobs;        // device array
+  int njobs;
+  int nin;                  // inputs per job (all jobs of a launch agree)
+  int nout;                 // outputs per job
+  int accumulate;           // 0: out = sum, 1: out ^= sum
+  int bytes_only;           // 1: a pointer is not 16-B aligned, use the byte path
+  int blocks_per_job;
+  size_t nbytes;            // bytes per cell
+};
+
+// XOR of `nin` inputs into one output (the XOR scheme's parity / rebuild).
+struct XorJob {
+  const uint8_t* in[kMaxIn];
+  uint8_t* out;
+};
+
+struct XorLaunch {
+  const XorJob* jobs;
+  int njobs;
+  int nin;
+  int accumulate;
+  int bytes_only;
+  int blocks_per_job;
+  size_t nbytes;
+};
+
+// launchers (codec_kernels.hip); return hipError_t as int
+int launch_gf(const GfLaunch& L, void* stream);
+int launch_xor(const XorLaunch& L, void* stream);
+// one job passed by value (L.jobs / L.njobs ignored; grid = blocks_per_job)
+int launch_gf_single(const GfLaunch& L, const GfJob& J, void* stream);
+int launch_xor_single(const XorLaunch& L, const XorJob& J, void* stream);
+// device properties used to size grids
+int device_cu_count();
+// occupancy of the GF kernel for a given input count (blocks per CU)
+int gf_blocks_per_cu(int nin);
+
+constexpr int kBlock = 256;
+
+}  // namespace redset_hip

@@ -1,0 +1,337 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the CPU oracle,
+bit-exact, plus size-independent properties at BASELINE.json's full sizes."""
+import itertools
+
+import numpy as np
+import pytest
+
+import np_ref
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def rd():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import redset_amd
+
+    redset_amd.load()
+    return redset_amd
+
+
+def upload_set(rd, lofi, parity, data_cells, parity_cells, chunk, padded=True):
+    p = len(lofi)
+    if padded:
+        lay = rd.SetLayout.allocate(p, data_cells, parity_cells, chunk)
+    else:  # cells packed back to back: unaligned whenever chunk % 16 != 0
+        lay = rd.SetLayout(p, data_cells, parity_cells, chunk, chunk,
+                           torch.empty(p * (data_cells + parity_cells) * chunk, dtype=torch.uint8, device="cuda"))
+    for r in range(p):
+        for s in range(data_cells):
+            lay.data_cell(r, s).copy_(torch.from_numpy(lofi[r][s * chunk:(s + 1) * chunk]))
+        for i in range(parity_cells):
+            lay.parity_cell(r, i).copy_(torch.from_numpy(parity[r][i * chunk:(i + 1) * chunk]))
+    torch.cuda.synchronize()
+    return lay
+
+
+def download_set(lay):
+    lofi, parity = [], []
+    for r in range(lay.ranks):
+        lofi.append(np.concatenate([lay.data_cell(r, s).cpu().numpy() for s in range(lay.data_cells)]))
+        parity.append(np.concatenate([lay.parity_cell(r, i).cpu().numpy() for i in range(lay.parity_cells)]))
+    return lofi, parity
+
+
+def gpu_bytes(arr: np.ndarray, offset=0):
+    """device copy of arr starting `offset` bytes into a fresh allocation"""
+    buf = torch.empty(arr.size + offset + 64, dtype=torch.uint8, device="cuda")
+    view = buf[offset: offset + arr.size]
+    view.copy_(torch.from_numpy(arr))
+    return buf, view
+
+
+# --------------------------------------------------------------------------
+# stripe primitives
+# --------------------------------------------------------------------------
+
+@pytest.mark.parametrize("nin,nout", [(1, 1), (2, 3), (8, 3), (8, 4), (16, 4), (13, 2), (5, 1)])
+@pytest.mark.parametrize("nbytes", [1, 15, 16, 17, 4096 + 7, (1 << 20) + 3])
+def test_gf_combine_matches_numpy(rd, nin, nout, nbytes):
+    rng = np.random.default_rng(nin * 100 + nout + nbytes)
+    ins = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(nin)]
+    coef = rng.integers(0, 256, (nout, nin), dtype=np.uint8)
+    coef[0, 0] = 0  # zero coefficient
+    if nin > 1:
+        coef[-1, 1] = 1  # identity coefficient
+    want = np.zeros((nout, nbytes), np.uint8)
+    for j in range(nout):
+        for i in range(nin):
+            want[j] ^= np_ref.MUL[coef[j, i], ins[i]]
+    d_in = [gpu_bytes(x)[1] for x in ins]
+    d_out = [torch.zeros(nbytes, dtype=torch.uint8, device="cuda") for _ in range(nout)]
+    rd.gf_combine(d_in, d_out, coef, nbytes)
+    torch.cuda.synchronize()
+    for j in range(nout):
+        assert np.array_equal(d_out[j].cpu().numpy(), want[j]), j
+    # accumulate: out ^= same sum -> zeros
+    rd.gf_combine(d_in, d_out, coef, nbytes, accumulate=True)
+    torch.cuda.synchronize()
+    for j in range(nout):
+        assert not d_out[j].any().item()
+
+
+@pytest.mark.parametrize("offset", [1, 3, 8])
+def test_gf_combine_unaligned(rd, offset):
+    nbytes = 100_003
+    rng = np.random.default_rng(offset)
+    ins = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(4)]
+    coef = rng.integers(1, 256, (3, 4), dtype=np.uint8)
+    want = np.zeros((3, nbytes), np.uint8)
+    for j in range(3):
+        for i in range(4):
+            want[j] ^= np_ref.MUL[coef[j, i], ins[i]]
+    d_in = [gpu_bytes(x, offset)[1] for x in ins]
+    outs = [gpu_bytes(np.zeros(nbytes, np.uint8), offset) for _ in range(3)]
+    rd.gf_combine(d_in, [o[1] for o in outs], coef, nbytes)
+    torch.cuda.synchronize()
+    for j in range(3):
+        assert np.array_equal(outs[j][1].cpu().numpy(), want[j])
+
+
+@pytest.mark.parametrize("nin", [1, 2, 7, 16])
+@pytest.mark.parametrize("nbytes,offset", [(33, 0), (1 << 20, 0), (5592406, 0), (4099, 5)])
+def test_xor_combine(rd, nin, nbytes, offset):
+    rng = np.random.default_rng(nin + nbytes)
+    ins = [rng.integers(0, 256, nbytes, dtype=np.uint8) for _ in range(nin)]
+    want = np.bitwise_xor.reduce(np.stack(ins), axis=0)
+    d_in = [gpu_bytes(x, offset)[1] for x in ins]
+    out = gpu_bytes(np.zeros(nbytes, np.uint8), offset)
+    rd.xor_combine(d_in, out[1], nbytes)
+    torch.cuda.synchronize()
+    assert np.array_equal(out[1].cpu().numpy(), want)
+
+
+# --------------------------------------------------------------------------
+# whole-set RS / XOR against the oracle
+# --------------------------------------------------------------------------
+
+RS_CASES = [
+    (4, 2, 4096),
+    (11, 3, 65536),       # config 3 shape, small chunk
+    (11, 3, 100_001),     # odd chunk: vector body + byte tail
+    (20, 4, 32768),       # config 5 shape (d = 16)
+    (8, 1, 20000),
+    (12, 6, 8192),        # e > 4: two output groups
+    (24, 4, 8192),        # d = 20 > 16: accumulate pass
+    (2, 1, 1000),
+]
+
+
+@pytest.mark.parametrize("p,e,chunk", RS_CASES)
+@pytest.mark.parametrize("padded", [True, False])
+def test_rs_encode_set(rd, oracle, p, e, chunk, padded):
+    lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=p * 1000 + e + chunk)
+    lay = upload_set(rd, lofi, parity, p - e, e, chunk, padded=padded)
+    codec = rd.RSCodec(p, e)
+    plan = codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    plan.execute()
+    torch.cuda.synchronize()
+    oracle.OracleRS(p, e).encode_set(lofi, parity, chunk)
+    _, got = download_set(lay)
+    for r in range(p):
+        assert np.array_equal(got[r], parity[r]), f"member {r}"
+    assert plan.bytes_read == p * (p - e) * chunk or (p - e) > 16
+    assert plan.bytes_written == p * e * chunk
+
+
+def _rebuild_case(rd, oracle, p, e, chunk, patterns, padded=True):
+    st = oracle.OracleRS(p, e)
+    lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=p + 7 * e + chunk)
+    st.encode_set(lofi, parity, chunk)
+    codec = rd.RSCodec(p, e)
+    lay = upload_set(rd, lofi, parity, p - e, e, chunk, padded=padded)
+    for lost in patterns:
+        for r in lost:  # erase (the rebuild must not read these)
+            lay.lofi(r).fill_(0xEE)
+            lay.parity(r).fill_(0xEE)
+        plan = codec.plan_rebuild(list(lost), lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+        plan.execute()
+        torch.cuda.synchronize()
+        # oracle: reference decode order on erased copies
+        lf = [x.copy() for x in lofi]
+        pr = [x.copy() for x in parity]
+        for r in lost:
+            lf[r][:] = 0
+            pr[r][:] = 0
+        assert st.rebuild_set(lost, lf, pr, chunk) == 0
+        gl, gp = download_set(lay)
+        for r in range(p):
+            assert np.array_equal(gl[r], lf[r]), (lost, r)
+            assert np.array_equal(gp[r], pr[r]), (lost, r)
+            # and the oracle reproduces the original
+            assert np.array_equal(lf[r], lofi[r]) and np.array_equal(pr[r], parity[r])
+
+
+@pytest.mark.parametrize("p,e", [(4, 2), (6, 3)])
+def test_rs_rebuild_every_pattern(rd, oracle, p, e):
+    pats = [c for m in range(1, e + 1) for c in itertools.combinations(range(p), m)]
+    _rebuild_case(rd, oracle, p, e, 4096 + 5, pats)
+
+
+@pytest.mark.parametrize("p,e,chunk,n", [(11, 3, 65536, 40), (20, 4, 16384, 12), (12, 6, 4096, 8),
+                                         (24, 4, 4096, 6)])
+def test_rs_rebuild_sampled_patterns(rd, oracle, p, e, chunk, n):
+    rng = np.random.default_rng(p * e)
+    pats = [(1, 2)] + [tuple(sorted(rng.choice(p, size=int(rng.integers(1, e + 1)), replace=False).tolist()))
+                       for _ in range(n)]
+    _rebuild_case(rd, oracle, p, e, chunk, pats)
+
+
+def test_rs_rebuild_unpadded_odd_chunk(rd, oracle):
+    _rebuild_case(rd, oracle, 11, 3, 5592406 // 64, [(0, 10), (3,), (2, 5, 7)], padded=False)
+
+
+def test_rs_rebuild_too_many_fails(rd):
+    codec = rd.RSCodec(6, 2)
+    lay = rd.SetLayout.allocate(6, 4, 2, 1024)
+    with pytest.raises(rd.RedsetHipError):
+        codec.plan_rebuild([0, 1, 2], lay.lofi_ptrs(), lay.parity_ptrs(), 1024, lay.cell_stride)
+
+
+@pytest.mark.parametrize("p,chunk,padded", [(4, 5592406, False), (4, 5592406, True), (8, 1 << 20, True),
+                                            (20, 10007, True), (2, 77, False)])
+def test_xor_encode_and_rebuild(rd, oracle, p, chunk, padded):
+    lofi, xorc = oracle.random_set(p, p - 1, 1, chunk, seed=p * chunk)
+    lay = upload_set(rd, lofi, xorc, p - 1, 1, chunk, padded=padded)
+    plan = rd.xor_plan_encode(p, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    plan.execute()
+    torch.cuda.synchronize()
+    oracle.xor_encode_set(p, lofi, xorc, chunk)
+    _, got = download_set(lay)
+    for r in range(p):
+        assert np.array_equal(got[r], xorc[r])
+    for root in sorted({0, p - 1, p // 2}):
+        lay.lofi(root).fill_(0x11)
+        lay.parity(root).fill_(0x22)
+        reb = rd.xor_plan_rebuild(p, root, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+        reb.execute()
+        torch.cuda.synchronize()
+        gl, gp = download_set(lay)
+        assert np.array_equal(gl[root], lofi[root]) and np.array_equal(gp[root], xorc[root])
+
+
+def test_plan_replays_in_cuda_graph(rd, oracle):
+    p, e, chunk = 11, 3, 1 << 16
+    lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=5)
+    lay = upload_set(rd, lofi, parity, p - e, e, chunk)
+    plan = rd.RSCodec(p, e).plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        plan.execute(s)  # warm-up outside capture
+    torch.cuda.current_stream().wait_stream(s)
+    for r in range(p):
+        lay.parity(r).zero_()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        plan.execute(torch.cuda.current_stream())
+    g.replay()
+    torch.cuda.synchronize()
+    oracle.OracleRS(p, e).encode_set(lofi, parity, chunk)
+    _, got = download_set(lay)
+    assert all(np.array_equal(a, b) for a, b in zip(got, parity))
+
+
+# --------------------------------------------------------------------------
+# BASELINE.json full sizes: size-independent properties
+# --------------------------------------------------------------------------
+
+def _fill_random(lay, seed):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    for r in range(lay.ranks):
+        lay.lofi(r).copy_(torch.randint(0, 256, (lay.lofi(r).numel(),), dtype=torch.uint8, device="cuda",
+                                        generator=g))
+
+
+def _window_check(oracle, lay, p, e, windows, rng):
+    """Parity is byte-wise: any byte window of the full-size parity must equal
+    the oracle's parity of the same window of the inputs."""
+    st = oracle.OracleRS(p, e)
+    C = lay.chunk_size
+    for _ in range(windows):
+        w = int(rng.integers(1, 4096))
+        off = int(rng.integers(0, C - w))
+        lofi = [np.concatenate([lay.data_cell(r, s)[off:off + w].cpu().numpy() for s in range(p - e)])
+                for r in range(p)]
+        parity = [np.zeros(e * w, np.uint8) for _ in range(p)]
+        st.encode_set(lofi, parity, w)
+        for r in range(p):
+            got = np.concatenate([lay.parity_cell(r, i)[off:off + w].cpu().numpy() for i in range(e)])
+            assert np.array_equal(got, parity[r]), (r, off, w)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("p,e,chunk", [(11, 3, 64 << 20), (20, 4, 64 << 20)])
+def test_full_size_encode_windows_and_round_trip(rd, oracle, p, e, chunk):
+    lay = rd.SetLayout.allocate(p, p - e, e, chunk)
+    _fill_random(lay, seed=p * e)
+    codec = rd.RSCodec(p, e)
+    codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride).execute()
+    torch.cuda.synchronize()
+    _window_check(oracle, lay, p, e, 12, np.random.default_rng(p))
+    # checksum of checksums before erasure
+    ref = lay.storage.clone()
+    lost = [1, 2] if e < 4 else [0, 5, 13, 19]
+    for r in lost:
+        lay.lofi(r).fill_(0)
+        lay.parity(r).fill_(0)
+    codec.plan_rebuild(lost, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride).execute()
+    torch.cuda.synchronize()
+    assert torch.equal(lay.storage, ref)
+
+
+@pytest.mark.slow
+def test_full_size_encode_is_linear(rd):
+    p, e, chunk = 11, 3, 64 << 20
+    codec = rd.RSCodec(p, e)
+    A = rd.SetLayout.allocate(p, p - e, e, chunk)
+    B = rd.SetLayout.allocate(p, p - e, e, chunk)
+    _fill_random(A, 1)
+    _fill_random(B, 2)
+    for L in (A, B):
+        codec.plan_encode(L.lofi_ptrs(), L.parity_ptrs(), chunk, L.cell_stride).execute()
+    pa = torch.cat([A.parity(r) for r in range(p)]).clone()
+    pb = torch.cat([B.parity(r) for r in range(p)]).clone()
+    for r in range(p):
+        A.lofi(r).bitwise_xor_(B.lofi(r))
+    codec.plan_encode(A.lofi_ptrs(), A.parity_ptrs(), chunk, A.cell_stride).execute()
+    torch.cuda.synchronize()
+    pab = torch.cat([A.parity(r) for r in range(p)])
+    assert torch.equal(pab, pa ^ pb)
+
+
+@pytest.mark.slow
+def test_full_size_xor_c2(rd, oracle):
+    p, chunk = 8, 64 << 20
+    lay = rd.SetLayout.allocate(p, p - 1, 1, chunk)
+    _fill_random(lay, 3)
+    rd.xor_plan_encode(p, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride).execute()
+    torch.cuda.synchronize()
+    # XOR of all cells of a stripe (data + parity) is zero, for every stripe
+    for c in range(p):
+        acc = lay.parity_cell(c, 0).clone()
+        for s in range(p):
+            if s != c:
+                acc ^= lay.data_cell(s, c if c < s else c - 1)
+        assert not acc.any().item()
+    ref = lay.storage.clone()
+    lay.lofi(3).fill_(0)
+    lay.parity(3).fill_(0)
+    rd.xor_plan_rebuild(p, 3, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride).execute()
+    torch.cuda.synchronize()
+    assert torch.equal(lay.storage, ref)

@@ -1,0 +1,33 @@
+#!/bin/bash
+# One GPU-box session: GPU tests, smoke, bench, rocprofv3 kernel stats.
+# Stops at the first step that faults / aborts / times out (exit >= 2 or
+# signal), per the pool rules; an ordinary test failure (exit 1) continues.
+# usage: tools/gpu_session.sh <tag> [pytest-args...]
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-run}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+ok() { local s=$1; [ "$s" -eq 0 ] || [ "$s" -eq 1 ]; }
+
+echo "== gpu tests" | tee "$OUT/progress.txt"
+timeout -k 10 900 python -m pytest tests -m gpu -q -x "$@" > "$OUT/gpu_tests.log" 2>&1
+s=$?; echo "gpu tests exit $s" | tee -a "$OUT/progress.txt"; tail -3 "$OUT/gpu_tests.log"
+ok $s || exit $s
+
+echo "== smoke" | tee -a "$OUT/progress.txt"
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+s=$?; echo "smoke exit $s" | tee -a "$OUT/progress.txt"; tail -2 "$OUT/smoke.log"
+ok $s || exit $s
+
+echo "== bench" | tee -a "$OUT/progress.txt"
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 > "$OUT/bench.json" 2> "$OUT/bench.err"
+s=$?; echo "bench exit $s" | tee -a "$OUT/progress.txt"; cat "$OUT/bench.json"; tail -3 "$OUT/bench.err"
+ok $s || exit $s
+
+echo "== rocprofv3 kernel stats" | tee -a "$OUT/progress.txt"
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
+  python3 bench.py --steps 20 --warmup 3 --cpu-baseline 0 > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+s=$?; echo "rocprof exit $s" | tee -a "$OUT/progress.txt"
+ok $s || exit $s
+echo "== done" | tee -a "$OUT/progress.txt"

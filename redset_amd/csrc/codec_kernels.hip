@@ -97,10 +97,12 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
   build_tables(lds, J, NIN, nout);
   __syncthreads();
 
+  // The job's blocks sweep its cells together, block-interleaved: at any
+  // moment they cover one contiguous window of every cell, which keeps HBM
+  // row locality across the ~100 concurrent cell streams (measured +8% over
+  // one contiguous range per block, tools/gfbench.hip "GS").
   const size_t nvec = L.bytes_only ? 0 : L.nbytes / 16;
-  const size_t per = (nvec + L.blocks_per_job - 1) / L.blocks_per_job;
-  const size_t v0 = per * part;
-  const size_t v1 = (v0 + per < nvec) ? v0 + per : nvec;
+  const size_t vstep = static_cast<size_t>(L.blocks_per_job) * kBlock;
 
   const uint4* in[NIN];
 #pragma unroll
@@ -109,7 +111,7 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
 #pragma unroll
   for (int j = 0; j < kMaxOut; ++j) out[j] = reinterpret_cast<uint4*>(J.out[j]);
 
-  for (size_t v = v0 + threadIdx.x; v < v1; v += kBlock) {
+  for (size_t v = static_cast<size_t>(part) * kBlock + threadIdx.x; v < nvec; v += vstep) {
     uint4 x[NIN];
 #pragma unroll
     for (int i = 0; i < NIN; ++i) x[i] = in[i][v];
@@ -175,14 +177,12 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
 template <int NIN>
 __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, int part) {
   const size_t nvec = L.bytes_only ? 0 : L.nbytes / 16;
-  const size_t per = (nvec + L.blocks_per_job - 1) / L.blocks_per_job;
-  const size_t v0 = per * part;
-  const size_t v1 = (v0 + per < nvec) ? v0 + per : nvec;
+  const size_t vstep = static_cast<size_t>(L.blocks_per_job) * kBlock;
   const uint4* in[NIN];
 #pragma unroll
   for (int i = 0; i < NIN; ++i) in[i] = reinterpret_cast<const uint4*>(J.in[i]);
   uint4* out = reinterpret_cast<uint4*>(J.out);
-  for (size_t v = v0 + threadIdx.x; v < v1; v += kBlock) {
+  for (size_t v = static_cast<size_t>(part) * kBlock + threadIdx.x; v < nvec; v += vstep) {
     uint4 x[NIN];
 #pragma unroll
     for (int i = 0; i < NIN; ++i) x[i] = in[i][v];

@@ -14,6 +14,7 @@
 #include <algorithm>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <new>
@@ -79,9 +80,23 @@ struct Stripe {
   std::vector<Target> targets;
 };
 
+// Resident 256-thread blocks per CU the codec aims for. HBM streams best at
+// low occupancy here: 2 blocks (8 waves) per CU beat 4 and 8 by 3-5% on
+// gf_mac, as fewer blocks beat more on a plain copy (tools/gfbench.hip,
+// tools/membench.hip); REDSET_HIP_BLOCKS_PER_CU overrides it.
+int target_blocks_per_cu(int occupancy) {
+  static int env = -1;
+  if (env < 0) {
+    const char* s = std::getenv("REDSET_HIP_BLOCKS_PER_CU");
+    env = (s && std::atoi(s) > 0) ? std::atoi(s) : 0;
+  }
+  const int want = env > 0 ? env : 2;
+  return std::max(1, std::min(want, occupancy));
+}
+
 // Blocks per job so the whole launch fits in one resident wave of blocks.
-int blocks_per_job(int njobs, size_t nbytes, int blocks_per_cu) {
-  const long target = static_cast<long>(redset_hip::device_cu_count()) * blocks_per_cu;
+int blocks_per_job(int njobs, size_t nbytes, int occupancy) {
+  const long target = static_cast<long>(redset_hip::device_cu_count()) * target_blocks_per_cu(occupancy);
   long bpj = std::max<long>(1, target / std::max(1, njobs));
   // at least one 16-B vector per thread per block
   const long vec_blocks = static_cast<long>((nbytes / 16 + redset_hip::kBlock - 1) / redset_hip::kBlock);

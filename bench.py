@@ -137,8 +137,6 @@ def main():
         runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank)
         step = runner.step
         bytes_per_step = runner.algorithmic_bytes * world
-        enc_plan = runner.local_encode_plan
-        reb_plan = runner.local_rebuild_plan
     else:
         codec = redset_amd.RSCodec(p, e)
         lay = redset_amd.SetLayout.allocate(p, d, e, chunk)
@@ -218,6 +216,9 @@ def main():
         eb = enc_plan.bytes_read + enc_plan.bytes_written
         rb = reb_plan.bytes_read + reb_plan.bytes_written
         achieved = (eb + rb) / ((enc_ms + reb_ms) * 1e-3) / 1e9
+        # PMC-measured HBM bytes per gf_mac launch, averaged over the step's
+        # encode and rebuild launches (tools/pmc_traffic.py; gfx950 FETCH_SIZE
+        # doubled); compare with the algorithmic average below
         traffic = load_traffic(args.traffic_json, "gf_mac_kernel<8>")
         result["roofline"] = {
             "bound": "hbm",
@@ -227,7 +228,8 @@ def main():
             "unit": "GB/s",
             "frac": round(achieved / HBM_PEAK_GBPS, 4),
             "traffic": traffic,
-            "algorithmic_bytes_per_launch": {"encode": eb, "rebuild": rb},
+            "algorithmic_bytes_per_launch": {"encode": eb, "rebuild": rb, "mean": (eb + rb) // 2},
+            "traffic_source": "profiles/traffic_latest.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
             "avg_launch_ms": {"encode": round(enc_ms, 4), "rebuild": round(reb_ms, 4)},
         }
         result["breakdown"] = {

@@ -338,3 +338,26 @@ def test_full_size_xor_c2(rd, oracle):
     rd.xor_plan_rebuild(p, 3, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride).execute()
     torch.cuda.synchronize()
     assert torch.equal(lay.storage, ref)
+
+
+def test_sharded_runner_world1_hip(rd, oracle):
+    """redset_amd.dist with the HIP backend at world size 1 (no exchange):
+    column-slab layout + plans over gathered slices, checked against the oracle."""
+    from redset_amd.dist import ShardedSetRunner
+
+    p, e, chunk = 11, 3, 300_000
+    run = ShardedSetRunner(p, e, chunk, [1, 2], world=1, rank=0, seed=3)
+    data = run.D_host.cpu().numpy()
+    run.encode()
+    torch.cuda.synchronize()
+    par = run.P_host.cpu().numpy()
+    lofi = [np.ascontiguousarray(data[0, r, :, :chunk]).reshape(-1) for r in range(p)]
+    want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+    oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    for r in range(p):
+        assert np.array_equal(np.ascontiguousarray(par[0, r, :, :chunk]).reshape(-1), want[r])
+    run.erase()
+    run.rebuild()
+    torch.cuda.synchronize()
+    assert np.array_equal(run.D_host.cpu().numpy()[..., :chunk], data[..., :chunk])
+    assert np.array_equal(run.P_host.cpu().numpy()[..., :chunk], par[..., :chunk])

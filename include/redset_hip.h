@@ -136,6 +136,75 @@ int redset_hip_xor_combine(const unsigned char* const* in, int nin, unsigned cha
 int redset_hip_rs_decode_matrix(const redset_hip_rs* rs, int missing, const int* rebuild_ranks,
                                 int chunk_id, unsigned char* coef_out);
 
+/* ---- host-resident streaming pipeline (pinned staging <-> HBM) ------- */
+/*
+ * Encode / rebuild a set whose cells live outside the GPU (host memory or
+ * files): cells stream through pinned host buffers, hipMemcpyAsync to HBM,
+ * the gf_mac / xor kernel, and back, with reads, H2D, compute, D2H and writes
+ * of successive (stripe, slice) units overlapped. This is the shape of the
+ * reference's own loop -- slices of redset_mpi_buf_size read via
+ * redset_lofi_pread, combined, written after the header
+ * (src/redset_reedsolomon.c:309-391) -- with the arithmetic on the GPU.
+ */
+#define REDSET_HIP_CELL_DATA (0)    /* logical-file segment `index` */
+#define REDSET_HIP_CELL_PARITY (1)  /* redundancy slot `index` */
+
+typedef struct {
+  /* Read / write `len` bytes at byte `offset` of a cell of member `rank`
+   * (kind DATA: logical-file offset index*chunk_size + offset; kind PARITY:
+   * redundancy-file offset header + index*chunk_size + offset). Return 0 on
+   * success. Called concurrently from the pipeline's I/O threads. */
+  int (*read)(void* ctx, int rank, int kind, int index, unsigned long long offset, size_t len, void* dst);
+  int (*write)(void* ctx, int rank, int kind, int index, unsigned long long offset, size_t len, const void* src);
+  void* ctx;
+} redset_hip_io;
+
+typedef struct {
+  double seconds;                    /* wall time of the call */
+  unsigned long long bytes_read;     /* algorithmic bytes of cells read */
+  unsigned long long bytes_written;  /* algorithmic bytes of cells written */
+  unsigned long long units;          /* (stripe, slice) units */
+  double read_seconds;               /* summed time inside io->read */
+  double write_seconds;              /* summed time inside io->write */
+  double gpu_seconds;                /* H2D + kernels + D2H, event-timed */
+} redset_hip_stream_stats;
+
+/* Stripes [first_stripe, first_stripe + nstripes) (nstripes <= 0: all).
+ * slice_bytes: per-cell slice (0 = 8 MiB); io_threads (0 = 8). */
+int redset_hip_rs_encode_stream(const redset_hip_rs* rs, size_t chunk_size, int first_stripe, int nstripes,
+                                size_t slice_bytes, int io_threads, const redset_hip_io* io,
+                                redset_hip_stream_stats* stats);
+int redset_hip_rs_rebuild_stream(const redset_hip_rs* rs, int missing, const int* rebuild_ranks, size_t chunk_size,
+                                 int first_stripe, int nstripes, size_t slice_bytes, int io_threads,
+                                 const redset_hip_io* io, redset_hip_stream_stats* stats);
+int redset_hip_xor_encode_stream(int ranks, size_t chunk_size, int first_stripe, int nstripes, size_t slice_bytes,
+                                 int io_threads, const redset_hip_io* io, redset_hip_stream_stats* stats);
+int redset_hip_xor_rebuild_stream(int ranks, int root, size_t chunk_size, int first_stripe, int nstripes,
+                                  size_t slice_bytes, int io_threads, const redset_hip_io* io,
+                                  redset_hip_stream_stats* stats);
+
+/* Built-in I/O over host memory laid out like the device set layout
+ * (lofi[r] + s*cell_stride, parity[r] + i*cell_stride). */
+typedef struct redset_hip_hostio redset_hip_hostio;
+int redset_hip_hostio_create(int ranks, unsigned char* const* lofi, unsigned char* const* parity, size_t cell_stride,
+                             redset_hip_io* io_out, redset_hip_hostio** out);
+void redset_hip_hostio_destroy(redset_hip_hostio* h);
+
+/* Built-in I/O over files with redset's logical-file semantics
+ * (src/redset_lofi.c:30-173): member r's logical file is the concatenation
+ * of its nfiles[r] data files (paths/sizes flattened member by member);
+ * reads past a file's recorded size return zeros, writes past it are
+ * dropped. Member r's parity goes to redundancy_paths[r] at
+ * header_sizes[r] + slot*chunk_size (src/redset_reedsolomon.c:380-381).
+ * Data files of members with writable[r] != 0 are created / extended to their
+ * recorded size (rebuild targets); other data files are opened read-only. */
+typedef struct redset_hip_fileio redset_hip_fileio;
+int redset_hip_fileio_create(int ranks, const int* nfiles, const char* const* paths,
+                             const unsigned long long* sizes, const char* const* redundancy_paths,
+                             const unsigned long long* header_sizes, size_t chunk_size, const int* writable,
+                             redset_hip_io* io_out, redset_hip_fileio** out);
+void redset_hip_fileio_destroy(redset_hip_fileio* f);
+
 /* Text of the last failure on this thread ("" if none). */
 const char* redset_hip_last_error(void);
 /* Library version string. */

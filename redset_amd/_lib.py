@@ -40,6 +40,14 @@ EXPORTED_SYMBOLS = (
     "redset_hip_rs_decode_matrix",
     "redset_hip_last_error",
     "redset_hip_version",
+    "redset_hip_rs_encode_stream",
+    "redset_hip_rs_rebuild_stream",
+    "redset_hip_xor_encode_stream",
+    "redset_hip_xor_rebuild_stream",
+    "redset_hip_hostio_create",
+    "redset_hip_hostio_destroy",
+    "redset_hip_fileio_create",
+    "redset_hip_fileio_destroy",
 )
 
 
@@ -65,7 +73,30 @@ class PlanInfo(ctypes.Structure):
     ]
 
 
+class StreamIO(ctypes.Structure):
+    """redset_hip_io: read/write callbacks + context (opaque here)."""
+
+    _fields_ = [("read", c_void_p), ("write", c_void_p), ("ctx", c_void_p)]
+
+
+class StreamStats(ctypes.Structure):
+    _fields_ = [
+        ("seconds", ctypes.c_double),
+        ("bytes_read", c_ulonglong),
+        ("bytes_written", c_ulonglong),
+        ("units", c_ulonglong),
+        ("read_seconds", ctypes.c_double),
+        ("write_seconds", ctypes.c_double),
+        ("gpu_seconds", ctypes.c_double),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 _PP = POINTER(c_void_p)
+_IOP = POINTER(StreamIO)
+_STP = POINTER(StreamStats)
 
 _SIGNATURES = {
     "redset_hip_rs_create": (c_int, [c_int, c_int, POINTER(c_void_p)]),
@@ -86,6 +117,19 @@ _SIGNATURES = {
     "redset_hip_gf_combine": (c_int, [_PP, c_int, _PP, c_int, POINTER(c_ubyte), c_size_t, c_int, c_void_p]),
     "redset_hip_xor_combine": (c_int, [_PP, c_int, c_void_p, c_size_t, c_int, c_void_p]),
     "redset_hip_rs_decode_matrix": (c_int, [c_void_p, c_int, POINTER(c_int), c_int, POINTER(c_ubyte)]),
+    "redset_hip_rs_encode_stream": (c_int, [c_void_p, c_size_t, c_int, c_int, c_size_t, c_int, _IOP, _STP]),
+    "redset_hip_rs_rebuild_stream": (
+        c_int, [c_void_p, c_int, POINTER(c_int), c_size_t, c_int, c_int, c_size_t, c_int, _IOP, _STP]),
+    "redset_hip_xor_encode_stream": (c_int, [c_int, c_size_t, c_int, c_int, c_size_t, c_int, _IOP, _STP]),
+    "redset_hip_xor_rebuild_stream": (c_int, [c_int, c_int, c_size_t, c_int, c_int, c_size_t, c_int, _IOP, _STP]),
+    "redset_hip_hostio_create": (c_int, [c_int, _PP, _PP, c_size_t, _IOP, POINTER(c_void_p)]),
+    "redset_hip_hostio_destroy": (None, [c_void_p]),
+    "redset_hip_fileio_create": (
+        c_int,
+        [c_int, POINTER(c_int), POINTER(c_char_p), POINTER(c_ulonglong), POINTER(c_char_p), POINTER(c_ulonglong),
+         c_size_t, POINTER(c_int), _IOP, POINTER(c_void_p)],
+    ),
+    "redset_hip_fileio_destroy": (None, [c_void_p]),
     "redset_hip_last_error": (c_char_p, []),
     "redset_hip_version": (c_char_p, []),
 }

@@ -4,7 +4,7 @@
 // A plan turns the reference's per-rank, per-slice loops (encode:
 // src/redset_reedsolomon.c:309-391, decode: :631-768, XOR: src/redset_xor.c:
 // 243-288, src/redset_xor_serial.c:202-273) into a few kernel launches over
-// whole cells: one GfJob per stripe, each reading its input cells once and
+// whole cells: one job per stripe, each reading its input cells once and
 // writing its output cells once. Planning happens once on the host; execute
 // only enqueues kernels, so it can be captured into a hipGraph.
 #include "redset_hip.h"
@@ -12,31 +12,26 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
-#include <cstdarg>
-#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <map>
 #include <new>
-#include <string>
 #include <tuple>
 #include <vector>
 
 #include "codec_kernels.h"
 #include "gf256.h"
+#include "stripe_map.h"
 
+using redset_hip::CellRef;
+using redset_hip::fail;
 using redset_hip::GfJob;
 using redset_hip::GfLaunch;
 using redset_hip::kMaxIn;
 using redset_hip::kMaxOut;
+using redset_hip::StripeMap;
 using redset_hip::XorJob;
 using redset_hip::XorLaunch;
-
-struct redset_hip_rs {
-  int ranks;
-  int encoding;
-  std::vector<uint8_t> mat;  // (p+e) x p
-};
 
 struct redset_hip_plan {
   redset_hip_plan_info info{};
@@ -48,19 +43,6 @@ struct redset_hip_plan {
 
 namespace {
 
-thread_local std::string g_err;
-
-int fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
-int fail(const char* fmt, ...) {
-  char buf[512];
-  va_list ap;
-  va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
-  va_end(ap);
-  g_err = buf;
-  return REDSET_FAILURE;
-}
-
 int hip_check(hipError_t e, const char* what) {
   if (e == hipSuccess) return REDSET_SUCCESS;
   return fail("%s: %s", what, hipGetErrorString(e));
@@ -68,35 +50,26 @@ int hip_check(hipError_t e, const char* what) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// One output cell of a stripe and its coefficient over each input of the stripe.
-struct Target {
-  uint8_t* cell;
-  std::vector<uint8_t> coef;  // one per stripe input
-};
-
-// A stripe's linear map: targets = coef * inputs.
-struct Stripe {
-  std::vector<const uint8_t*> inputs;
-  std::vector<Target> targets;
-};
-
 // Resident 256-thread blocks per CU the codec aims for. HBM streams best at
-// low occupancy here: 2 blocks (8 waves) per CU beat 4 and 8 by 3-5% on
-// gf_mac, as fewer blocks beat more on a plain copy (tools/gfbench.hip,
-// tools/membench.hip); REDSET_HIP_BLOCKS_PER_CU overrides it.
+// moderate occupancy here: with the software-pipelined gf_mac, 4 blocks
+// (16 waves) per CU beat 2, 3 and 8 (tools/gfbench.hip "PIPE"; a plain copy
+// also prefers few blocks, tools/membench.hip); REDSET_HIP_BLOCKS_PER_CU
+// overrides it.
 int target_blocks_per_cu(int occupancy) {
   static int env = -1;
   if (env < 0) {
     const char* s = std::getenv("REDSET_HIP_BLOCKS_PER_CU");
     env = (s && std::atoi(s) > 0) ? std::atoi(s) : 0;
   }
-  const int want = env > 0 ? env : 2;
+  const int want = env > 0 ? env : 4;
   return std::max(1, std::min(want, occupancy));
 }
 
 // Blocks per job so the whole launch fits in one resident wave of blocks.
-int blocks_per_job(int njobs, size_t nbytes, int occupancy) {
-  const long target = static_cast<long>(redset_hip::device_cu_count()) * target_blocks_per_cu(occupancy);
+int blocks_per_job(int njobs, size_t nbytes, int occupancy, int blocks_total = 0) {
+  const long target = blocks_total > 0
+                          ? blocks_total
+                          : static_cast<long>(redset_hip::device_cu_count()) * target_blocks_per_cu(occupancy);
   long bpj = std::max<long>(1, target / std::max(1, njobs));
   // at least one 16-B vector per thread per block
   const long vec_blocks = static_cast<long>((nbytes / 16 + redset_hip::kBlock - 1) / redset_hip::kBlock);
@@ -104,143 +77,130 @@ int blocks_per_job(int njobs, size_t nbytes, int occupancy) {
   return static_cast<int>(bpj);
 }
 
-// Split stripes into launches of <= kMaxIn inputs x <= kMaxOut outputs.
+// Device address of a cell in the set layout of include/redset_hip.h.
+struct SetLayout {
+  unsigned char* const* lofi;
+  unsigned char* const* parity;
+  size_t stride;
+  uint8_t* at(const CellRef& c) const {
+    return (c.kind == redset_hip::kData ? lofi[c.rank] : parity[c.rank]) + static_cast<size_t>(c.index) * stride;
+  }
+};
+
+// Split stripe maps into launches of <= kMaxIn inputs x <= kMaxOut outputs.
 // Output groups are independent; input groups of one output group run in
-// order, the first overwriting and the rest accumulating. Stripes with equal
-// input counts share a launch.
-int build_gf_plan(redset_hip_plan* plan, const std::vector<Stripe>& stripes, size_t nbytes) {
-  struct Pending {
+// order, the first overwriting and the rest accumulating. Jobs with equal
+// shapes share a launch. XOR maps go to the XOR kernel.
+int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const SetLayout& L, size_t nbytes) {
+  struct GfPending {
     std::vector<GfJob> jobs;
     int nin, nout, accumulate, bytes_only;
   };
-  std::map<std::tuple<int, int, int, int>, Pending> groups;  // (ig, nin, nout, og) ordering key
+  struct XorPending {
+    std::vector<XorJob> jobs;
+    int nin, accumulate, bytes_only;
+  };
+  std::map<std::tuple<int, int, int, int>, GfPending> gf;  // (input group, nin, nout, unaligned)
+  std::map<std::tuple<int, int, int>, XorPending> xr;      // (input group, nin, unaligned)
   unsigned long long rd = 0, wr = 0;
-  for (const Stripe& s : stripes) {
-    const int nin = static_cast<int>(s.inputs.size());
-    const int nt = static_cast<int>(s.targets.size());
+  for (const StripeMap& m : maps) {
+    const int nin = static_cast<int>(m.in.size());
+    const int nt = static_cast<int>(m.out.size());
     if (nt == 0) continue;
     if (nin == 0) return fail("stripe with outputs but no inputs");
     for (int og = 0; og * kMaxOut < nt; ++og) {
       const int o0 = og * kMaxOut, no = std::min(kMaxOut, nt - o0);
+      if (m.xor_only && no != 1) return fail("XOR stripe with %d outputs", no);
       for (int ig = 0; ig * kMaxIn < nin; ++ig) {
         const int i0 = ig * kMaxIn, ni = std::min(kMaxIn, nin - i0);
+        bool al = true;
+        rd += static_cast<unsigned long long>(ni + (ig > 0 ? no : 0)) * nbytes;
+        wr += static_cast<unsigned long long>(no) * nbytes;
+        if (m.xor_only) {
+          XorJob J;
+          std::memset(&J, 0, sizeof(J));
+          for (int i = 0; i < ni; ++i) {
+            J.in[i] = L.at(m.in[i0 + i]);
+            al = al && aligned16(J.in[i]);
+          }
+          J.out = L.at(m.out[o0]);
+          al = al && aligned16(J.out);
+          XorPending& P = xr[std::make_tuple(ig, ni, al ? 0 : 1)];
+          P.nin = ni;
+          P.accumulate = ig > 0;
+          P.bytes_only = al ? 0 : 1;
+          P.jobs.push_back(J);
+          continue;
+        }
         GfJob J;
         std::memset(&J, 0, sizeof(J));
-        bool al = true;
         for (int i = 0; i < ni; ++i) {
-          J.in[i] = s.inputs[i0 + i];
+          J.in[i] = L.at(m.in[i0 + i]);
           al = al && aligned16(J.in[i]);
         }
         for (int j = 0; j < no; ++j) {
-          J.out[j] = s.targets[o0 + j].cell;
+          J.out[j] = L.at(m.out[o0 + j]);
           al = al && aligned16(J.out[j]);
-          for (int i = 0; i < ni; ++i) J.coef[j][i] = s.targets[o0 + j].coef[i0 + i];
+          for (int i = 0; i < ni; ++i) J.coef[j][i] = m.coef[static_cast<size_t>(o0 + j) * nin + i0 + i];
         }
-        Pending& P = groups[std::make_tuple(ig, ni, no, al ? 0 : 1)];
+        GfPending& P = gf[std::make_tuple(ig, ni, no, al ? 0 : 1)];
         P.nin = ni;
         P.nout = no;
         P.accumulate = ig > 0;
         P.bytes_only = al ? 0 : 1;
         P.jobs.push_back(J);
-        rd += static_cast<unsigned long long>(ni + (ig > 0 ? no : 0)) * nbytes;
-        wr += static_cast<unsigned long long>(no) * nbytes;
       }
     }
   }
-  size_t total = 0;
-  for (auto& kv : groups) total += kv.second.jobs.size();
-  plan->info.jobs = static_cast<int>(total);
   plan->info.bytes_read = rd;
   plan->info.bytes_written = wr;
-  if (total == 0) return REDSET_SUCCESS;
-  std::vector<GfJob> all;
-  all.reserve(total);
-  for (auto& kv : groups) {
-    Pending& P = kv.second;
-    GfLaunch L;
-    std::memset(&L, 0, sizeof(L));
-    L.jobs = reinterpret_cast<const GfJob*>(all.size());  // offset, patched below
-    L.njobs = static_cast<int>(P.jobs.size());
-    L.nin = P.nin;
-    L.nout = P.nout;
-    L.accumulate = P.accumulate;
-    L.bytes_only = P.bytes_only;
-    L.nbytes = nbytes;
-    L.blocks_per_job = blocks_per_job(L.njobs, nbytes, redset_hip::gf_blocks_per_cu(P.nin));
-    all.insert(all.end(), P.jobs.begin(), P.jobs.end());
-    plan->gf_launches.push_back(L);
+  std::vector<GfJob> gall;
+  std::vector<XorJob> xall;
+  for (auto& kv : gf) {
+    GfPending& P = kv.second;
+    GfLaunch G;
+    std::memset(&G, 0, sizeof(G));
+    G.jobs = reinterpret_cast<const GfJob*>(gall.size());  // offset, patched below
+    G.njobs = static_cast<int>(P.jobs.size());
+    G.nin = P.nin;
+    G.nout = P.nout;
+    G.accumulate = P.accumulate;
+    G.bytes_only = P.bytes_only;
+    G.nbytes = nbytes;
+    G.blocks_per_job = blocks_per_job(G.njobs, nbytes, redset_hip::gf_blocks_per_cu(P.nin));
+    gall.insert(gall.end(), P.jobs.begin(), P.jobs.end());
+    plan->gf_launches.push_back(G);
   }
-  if (int rc = hip_check(hipMalloc(&plan->d_gf, all.size() * sizeof(GfJob)), "hipMalloc(plan jobs)")) return rc;
-  if (int rc = hip_check(hipMemcpy(plan->d_gf, all.data(), all.size() * sizeof(GfJob), hipMemcpyHostToDevice),
-                         "hipMemcpy(plan jobs)"))
-    return rc;
-  for (GfLaunch& L : plan->gf_launches) L.jobs = plan->d_gf + reinterpret_cast<uintptr_t>(L.jobs);
-  plan->info.launches = static_cast<int>(plan->gf_launches.size());
-  return REDSET_SUCCESS;
-}
-
-// XOR stripes: output = XOR of inputs; > kMaxIn inputs accumulate in passes.
-struct XorStripe {
-  std::vector<const uint8_t*> inputs;
-  uint8_t* out;
-};
-
-int build_xor_plan(redset_hip_plan* plan, const std::vector<XorStripe>& stripes, size_t nbytes) {
-  struct Pending {
-    std::vector<XorJob> jobs;
-    int nin, accumulate, bytes_only;
-  };
-  std::map<std::tuple<int, int, int>, Pending> groups;
-  unsigned long long rd = 0, wr = 0;
-  for (const XorStripe& s : stripes) {
-    const int nin = static_cast<int>(s.inputs.size());
-    if (nin == 0) return fail("XOR stripe with no inputs");
-    for (int ig = 0; ig * kMaxIn < nin; ++ig) {
-      const int i0 = ig * kMaxIn, ni = std::min(kMaxIn, nin - i0);
-      XorJob J;
-      std::memset(&J, 0, sizeof(J));
-      bool al = aligned16(s.out);
-      for (int i = 0; i < ni; ++i) {
-        J.in[i] = s.inputs[i0 + i];
-        al = al && aligned16(J.in[i]);
-      }
-      J.out = s.out;
-      Pending& P = groups[std::make_tuple(ig, ni, al ? 0 : 1)];
-      P.nin = ni;
-      P.accumulate = ig > 0;
-      P.bytes_only = al ? 0 : 1;
-      P.jobs.push_back(J);
-      rd += static_cast<unsigned long long>(ni + (ig > 0 ? 1 : 0)) * nbytes;
-      wr += nbytes;
-    }
+  for (auto& kv : xr) {
+    XorPending& P = kv.second;
+    XorLaunch X;
+    std::memset(&X, 0, sizeof(X));
+    X.jobs = reinterpret_cast<const XorJob*>(xall.size());
+    X.njobs = static_cast<int>(P.jobs.size());
+    X.nin = P.nin;
+    X.accumulate = P.accumulate;
+    X.bytes_only = P.bytes_only;
+    X.nbytes = nbytes;
+    X.blocks_per_job = blocks_per_job(X.njobs, nbytes, 8);
+    xall.insert(xall.end(), P.jobs.begin(), P.jobs.end());
+    plan->xor_launches.push_back(X);
   }
-  size_t total = 0;
-  for (auto& kv : groups) total += kv.second.jobs.size();
-  plan->info.jobs = static_cast<int>(total);
-  plan->info.bytes_read = rd;
-  plan->info.bytes_written = wr;
-  if (total == 0) return REDSET_SUCCESS;
-  std::vector<XorJob> all;
-  for (auto& kv : groups) {
-    Pending& P = kv.second;
-    XorLaunch L;
-    std::memset(&L, 0, sizeof(L));
-    L.jobs = reinterpret_cast<const XorJob*>(all.size());
-    L.njobs = static_cast<int>(P.jobs.size());
-    L.nin = P.nin;
-    L.accumulate = P.accumulate;
-    L.bytes_only = P.bytes_only;
-    L.nbytes = nbytes;
-    L.blocks_per_job = blocks_per_job(L.njobs, nbytes, 8);
-    all.insert(all.end(), P.jobs.begin(), P.jobs.end());
-    plan->xor_launches.push_back(L);
+  plan->info.jobs = static_cast<int>(gall.size() + xall.size());
+  plan->info.launches = static_cast<int>(plan->gf_launches.size() + plan->xor_launches.size());
+  if (!gall.empty()) {
+    if (int rc = hip_check(hipMalloc(&plan->d_gf, gall.size() * sizeof(GfJob)), "hipMalloc(plan jobs)")) return rc;
+    if (int rc = hip_check(hipMemcpy(plan->d_gf, gall.data(), gall.size() * sizeof(GfJob), hipMemcpyHostToDevice),
+                           "hipMemcpy(plan jobs)"))
+      return rc;
+    for (GfLaunch& G : plan->gf_launches) G.jobs = plan->d_gf + reinterpret_cast<uintptr_t>(G.jobs);
   }
-  if (int rc = hip_check(hipMalloc(&plan->d_xor, all.size() * sizeof(XorJob)), "hipMalloc(plan jobs)")) return rc;
-  if (int rc = hip_check(hipMemcpy(plan->d_xor, all.data(), all.size() * sizeof(XorJob), hipMemcpyHostToDevice),
-                         "hipMemcpy(plan jobs)"))
-    return rc;
-  for (XorLaunch& L : plan->xor_launches) L.jobs = plan->d_xor + reinterpret_cast<uintptr_t>(L.jobs);
-  plan->info.launches = static_cast<int>(plan->xor_launches.size());
+  if (!xall.empty()) {
+    if (int rc = hip_check(hipMalloc(&plan->d_xor, xall.size() * sizeof(XorJob)), "hipMalloc(plan jobs)")) return rc;
+    if (int rc = hip_check(hipMemcpy(plan->d_xor, xall.data(), xall.size() * sizeof(XorJob), hipMemcpyHostToDevice),
+                           "hipMemcpy(plan jobs)"))
+      return rc;
+    for (XorLaunch& X : plan->xor_launches) X.jobs = plan->d_xor + reinterpret_cast<uintptr_t>(X.jobs);
+  }
   return REDSET_SUCCESS;
 }
 
@@ -255,59 +215,89 @@ int check_set_args(const void* const* a, const void* const* b, int ranks, size_t
   return REDSET_SUCCESS;
 }
 
-// cell of member `rank` in stripe `chunk`: a data segment in lofi or a
-// parity slot in the redundancy region
-uint8_t* rs_cell(const redset_hip_rs* rs, unsigned char* const* lofi, unsigned char* const* parity, int rank,
-                 int chunk, size_t stride) {
-  const int p = rs->ranks, e = rs->encoding;
-  const int enc = redset_hip::encoding_id(p, e, rank, chunk);
-  if (enc < p) return lofi[rank] + static_cast<size_t>(redset_hip::data_id(p, e, rank, chunk)) * stride;
-  return parity[rank] + static_cast<size_t>(enc - p) * stride;
-}
-
-// decode map of one stripe as (missing x p): column s = member s's cell
-int decode_map(const redset_hip_rs* rs, int missing, const int* rebuild_ranks, int chunk, std::vector<uint8_t>& D) {
-  const int p = rs->ranks, e = rs->encoding;
-  const redset_hip::Field& F = redset_hip::field();
-  std::vector<int> unknowns(missing);
-  std::vector<char> erased(p, 0);
-  for (int i = 0; i < missing; ++i) {
-    if (rebuild_ranks[i] < 0 || rebuild_ranks[i] >= p) return fail("rebuild rank %d out of range", rebuild_ranks[i]);
-    if (i > 0 && rebuild_ranks[i] <= rebuild_ranks[i - 1]) return fail("rebuild_ranks must be ascending");
-    erased[rebuild_ranks[i]] = 1;
-    unknowns[i] = redset_hip::encoding_id(p, e, rebuild_ranks[i], chunk);
+int finish_plan(int kind, int ranks, int encoding, int missing, size_t chunk, const std::vector<StripeMap>& maps,
+                const SetLayout& L, redset_hip_plan** out) {
+  redset_hip_plan* plan = new (std::nothrow) redset_hip_plan;
+  if (!plan) return fail("out of host memory");
+  plan->info.kind = kind;
+  plan->info.ranks = ranks;
+  plan->info.encoding = encoding;
+  plan->info.missing = missing;
+  plan->info.chunk_size = chunk;
+  if (int rc = build_plan(plan, maps, L, chunk)) {
+    redset_hip_plan_destroy(plan);
+    return rc;
   }
-  std::vector<uint8_t> m;
-  std::vector<int> rows;
-  redset_hip::identify_rows(rs->mat, p, e, missing, unknowns.data(), m, rows);
-  for (int i = 0; i < missing; ++i)
-    if (rows[i] < 0) return fail("no parity row available for unknown %d", i);
-  const std::vector<uint8_t> T = redset_hip::solve_transform(m, missing);
-  // accumulator k (redset_rs_reduce_decode, src/redset_reedsolomon_common.c:
-  // 855-899) = sum over surviving members s of a_k(s) * cell_s
-  D.assign(static_cast<size_t>(missing) * p, 0);
-  for (int s = 0; s < p; ++s) {
-    if (erased[s]) continue;
-    const int enc = redset_hip::encoding_id(p, e, s, chunk);
-    for (int k = 0; k < missing; ++k) {
-      const int row = rows[k] + p;
-      uint8_t a;
-      if (enc < p) a = rs->mat[static_cast<size_t>(row) * p + s];
-      else a = (enc == row) ? 1 : 0;
-      if (!a) continue;
-      for (int i = 0; i < missing; ++i)
-        D[static_cast<size_t>(i) * p + s] ^= F.mul(T[static_cast<size_t>(i) * missing + k], a);
-    }
-  }
+  *out = plan;
   return REDSET_SUCCESS;
 }
 
 }  // namespace
 
+namespace redset_hip {
+
+int run_stripe(const StripeMap& m, const uint8_t* const* in, uint8_t* const* out, size_t nbytes, void* stream,
+               int blocks_total) {
+  const int nin = static_cast<int>(m.in.size()), nt = static_cast<int>(m.out.size());
+  for (int og = 0; og * kMaxOut < nt; ++og) {
+    const int o0 = og * kMaxOut, no = std::min(kMaxOut, nt - o0);
+    for (int ig = 0; ig * kMaxIn < nin; ++ig) {
+      const int i0 = ig * kMaxIn, ni = std::min(kMaxIn, nin - i0);
+      bool al = true;
+      int e;
+      if (m.xor_only) {
+        XorJob J;
+        std::memset(&J, 0, sizeof(J));
+        for (int i = 0; i < ni; ++i) {
+          J.in[i] = in[i0 + i];
+          al = al && aligned16(J.in[i]);
+        }
+        J.out = out[o0];
+        al = al && aligned16(J.out);
+        XorLaunch X;
+        std::memset(&X, 0, sizeof(X));
+        X.njobs = 1;
+        X.nin = ni;
+        X.accumulate = ig > 0;
+        X.bytes_only = al ? 0 : 1;
+        X.nbytes = nbytes;
+        X.blocks_per_job = blocks_per_job(1, nbytes, 8, blocks_total);
+        e = launch_xor_single(X, J, stream);
+      } else {
+        GfJob J;
+        std::memset(&J, 0, sizeof(J));
+        for (int i = 0; i < ni; ++i) {
+          J.in[i] = in[i0 + i];
+          al = al && aligned16(J.in[i]);
+        }
+        for (int j = 0; j < no; ++j) {
+          J.out[j] = out[o0 + j];
+          al = al && aligned16(J.out[j]);
+          for (int i = 0; i < ni; ++i) J.coef[j][i] = m.coef[static_cast<size_t>(o0 + j) * nin + i0 + i];
+        }
+        GfLaunch G;
+        std::memset(&G, 0, sizeof(G));
+        G.njobs = 1;
+        G.nin = ni;
+        G.nout = no;
+        G.accumulate = ig > 0;
+        G.bytes_only = al ? 0 : 1;
+        G.nbytes = nbytes;
+        G.blocks_per_job = blocks_per_job(1, nbytes, gf_blocks_per_cu(ni), blocks_total);
+        e = launch_gf_single(G, J, stream);
+      }
+      if (e) return hip_check(static_cast<hipError_t>(e), "stripe kernel launch");
+    }
+  }
+  return REDSET_SUCCESS;
+}
+
+}  // namespace redset_hip
+
 extern "C" {
 
-const char* redset_hip_last_error(void) { return g_err.c_str(); }
-const char* redset_hip_version(void) { return "redset-hip 0.1 (gfx950)"; }
+const char* redset_hip_last_error(void) { return redset_hip::last_error(); }
+const char* redset_hip_version(void) { return "redset-hip 0.2 (gfx950)"; }
 
 int redset_hip_rs_create(int ranks, int encoding, redset_hip_rs** out) {
   if (!out) return fail("null out-pointer");
@@ -340,55 +330,26 @@ int redset_hip_rs_get_data_id(int ranks, int encoding, int rank, int chunk_id) {
   return redset_hip::data_id(ranks, encoding, rank, chunk_id);
 }
 
+int redset_hip_rs_decode_matrix(const redset_hip_rs* rs, int missing, const int* rebuild_ranks, int chunk_id,
+                                unsigned char* coef_out) {
+  if (!rs || !coef_out || !rebuild_ranks) return fail("null argument");
+  if (chunk_id < 0 || chunk_id >= rs->ranks) return fail("chunk id %d out of range", chunk_id);
+  std::vector<uint8_t> D;
+  if (int rc = redset_hip::rs_decode_matrix(rs, missing, rebuild_ranks, chunk_id, D)) return rc;
+  std::memcpy(coef_out, D.data(), D.size());
+  return REDSET_SUCCESS;
+}
+
 int redset_hip_rs_plan_encode(const redset_hip_rs* rs, unsigned char* const* lofi, unsigned char* const* parity,
                               size_t chunk_size, size_t stride, redset_hip_plan** out) {
   if (!rs) return fail("null rs state");
   if (int rc = check_set_args(reinterpret_cast<const void* const*>(lofi), reinterpret_cast<const void* const*>(parity),
                               rs->ranks, chunk_size, stride, out))
     return rc;
-  const int p = rs->ranks, e = rs->encoding;
-  std::vector<Stripe> stripes(p);
-  for (int c = 0; c < p; ++c) {
-    Stripe& S = stripes[c];
-    std::vector<int> data_ranks;
-    for (int s = 0; s < p; ++s) {
-      if (redset_hip::encoding_id(p, e, s, c) < p) {
-        data_ranks.push_back(s);
-        S.inputs.push_back(rs_cell(rs, lofi, parity, s, c, stride));
-      }
-    }
-    for (int r = 0; r < p; ++r) {
-      const int row = redset_hip::encoding_id(p, e, r, c);
-      if (row < p) continue;
-      Target t;
-      t.cell = parity[r] + static_cast<size_t>(row - p) * stride;
-      for (int s : data_ranks) t.coef.push_back(rs->mat[static_cast<size_t>(row) * p + s]);
-      S.targets.push_back(std::move(t));
-    }
-  }
-  redset_hip_plan* plan = new (std::nothrow) redset_hip_plan;
-  if (!plan) return fail("out of host memory");
-  plan->info.kind = REDSET_HIP_PLAN_RS_ENCODE;
-  plan->info.ranks = p;
-  plan->info.encoding = e;
-  plan->info.chunk_size = chunk_size;
-  if (int rc = build_gf_plan(plan, stripes, chunk_size)) {
-    redset_hip_plan_destroy(plan);
-    return rc;
-  }
-  *out = plan;
-  return REDSET_SUCCESS;
-}
-
-int redset_hip_rs_decode_matrix(const redset_hip_rs* rs, int missing, const int* rebuild_ranks, int chunk_id,
-                                unsigned char* coef_out) {
-  if (!rs || !coef_out || (missing > 0 && !rebuild_ranks)) return fail("null argument");
-  if (missing < 1 || missing > rs->encoding) return fail("cannot rebuild %d members with %d parity", missing, rs->encoding);
-  if (chunk_id < 0 || chunk_id >= rs->ranks) return fail("chunk id %d out of range", chunk_id);
-  std::vector<uint8_t> D;
-  if (int rc = decode_map(rs, missing, rebuild_ranks, chunk_id, D)) return rc;
-  std::memcpy(coef_out, D.data(), D.size());
-  return REDSET_SUCCESS;
+  std::vector<StripeMap> maps(rs->ranks);
+  for (int c = 0; c < rs->ranks; ++c) redset_hip::rs_encode_map(rs, c, maps[c]);
+  return finish_plan(REDSET_HIP_PLAN_RS_ENCODE, rs->ranks, rs->encoding, 0, chunk_size, maps,
+                     SetLayout{lofi, parity, stride}, out);
 }
 
 int redset_hip_rs_plan_rebuild(const redset_hip_rs* rs, int missing, const int* rebuild_ranks,
@@ -398,44 +359,17 @@ int redset_hip_rs_plan_rebuild(const redset_hip_rs* rs, int missing, const int* 
   if (int rc = check_set_args(reinterpret_cast<const void* const*>(lofi), reinterpret_cast<const void* const*>(parity),
                               rs->ranks, chunk_size, stride, out))
     return rc;
-  const int p = rs->ranks;
   if (missing < 0 || missing > rs->encoding)
     return fail("cannot rebuild %d members with %d parity chunks", missing, rs->encoding);
   if (missing > 0 && !rebuild_ranks) return fail("null rebuild_ranks");
-  std::vector<Stripe> stripes;
-  for (int c = 0; c < p && missing > 0; ++c) {
-    std::vector<uint8_t> D;
-    if (int rc = decode_map(rs, missing, rebuild_ranks, c, D)) return rc;
-    Stripe S;
-    std::vector<int> cols;
-    for (int s = 0; s < p; ++s) {
-      bool used = false;
-      for (int i = 0; i < missing; ++i) used = used || D[static_cast<size_t>(i) * p + s] != 0;
-      if (!used) continue;
-      cols.push_back(s);
-      S.inputs.push_back(rs_cell(rs, lofi, parity, s, c, stride));
-    }
-    for (int i = 0; i < missing; ++i) {
-      Target t;
-      t.cell = rs_cell(rs, lofi, parity, rebuild_ranks[i], c, stride);
-      for (int s : cols) t.coef.push_back(D[static_cast<size_t>(i) * p + s]);
-      S.targets.push_back(std::move(t));
-    }
-    stripes.push_back(std::move(S));
+  std::vector<StripeMap> maps;
+  for (int c = 0; c < rs->ranks && missing > 0; ++c) {
+    StripeMap m;
+    if (int rc = redset_hip::rs_rebuild_map(rs, missing, rebuild_ranks, c, m)) return rc;
+    maps.push_back(std::move(m));
   }
-  redset_hip_plan* plan = new (std::nothrow) redset_hip_plan;
-  if (!plan) return fail("out of host memory");
-  plan->info.kind = REDSET_HIP_PLAN_RS_REBUILD;
-  plan->info.ranks = p;
-  plan->info.encoding = rs->encoding;
-  plan->info.missing = missing;
-  plan->info.chunk_size = chunk_size;
-  if (int rc = build_gf_plan(plan, stripes, chunk_size)) {
-    redset_hip_plan_destroy(plan);
-    return rc;
-  }
-  *out = plan;
-  return REDSET_SUCCESS;
+  return finish_plan(REDSET_HIP_PLAN_RS_REBUILD, rs->ranks, rs->encoding, missing, chunk_size, maps,
+                     SetLayout{lofi, parity, stride}, out);
 }
 
 int redset_hip_xor_plan_encode(int ranks, unsigned char* const* lofi, unsigned char* const* xorc, size_t chunk_size,
@@ -444,26 +378,9 @@ int redset_hip_xor_plan_encode(int ranks, unsigned char* const* lofi, unsigned c
   if (int rc = check_set_args(reinterpret_cast<const void* const*>(lofi), reinterpret_cast<const void* const*>(xorc),
                               ranks, chunk_size, stride, out))
     return rc;
-  std::vector<XorStripe> stripes(ranks);
-  for (int c = 0; c < ranks; ++c) {
-    for (int s = 0; s < ranks; ++s) {
-      if (s == c) continue;
-      stripes[c].inputs.push_back(lofi[s] + static_cast<size_t>(redset_hip::xor_segment(s, c)) * stride);
-    }
-    stripes[c].out = xorc[c];
-  }
-  redset_hip_plan* plan = new (std::nothrow) redset_hip_plan;
-  if (!plan) return fail("out of host memory");
-  plan->info.kind = REDSET_HIP_PLAN_XOR_ENCODE;
-  plan->info.ranks = ranks;
-  plan->info.encoding = 1;
-  plan->info.chunk_size = chunk_size;
-  if (int rc = build_xor_plan(plan, stripes, chunk_size)) {
-    redset_hip_plan_destroy(plan);
-    return rc;
-  }
-  *out = plan;
-  return REDSET_SUCCESS;
+  std::vector<StripeMap> maps(ranks);
+  for (int c = 0; c < ranks; ++c) redset_hip::xor_encode_map(ranks, c, maps[c]);
+  return finish_plan(REDSET_HIP_PLAN_XOR_ENCODE, ranks, 1, 0, chunk_size, maps, SetLayout{lofi, xorc, stride}, out);
 }
 
 int redset_hip_xor_plan_rebuild(int ranks, int root, unsigned char* const* lofi, unsigned char* const* xorc,
@@ -473,38 +390,17 @@ int redset_hip_xor_plan_rebuild(int ranks, int root, unsigned char* const* lofi,
   if (int rc = check_set_args(reinterpret_cast<const void* const*>(lofi), reinterpret_cast<const void* const*>(xorc),
                               ranks, chunk_size, stride, out))
     return rc;
-  auto cell = [&](int s, int c) -> uint8_t* {
-    return s == c ? xorc[s] : lofi[s] + static_cast<size_t>(redset_hip::xor_segment(s, c)) * stride;
-  };
-  std::vector<XorStripe> stripes(ranks);
-  for (int c = 0; c < ranks; ++c) {
-    for (int s = 0; s < ranks; ++s)
-      if (s != root) stripes[c].inputs.push_back(cell(s, c));
-    stripes[c].out = cell(root, c);
-  }
-  redset_hip_plan* plan = new (std::nothrow) redset_hip_plan;
-  if (!plan) return fail("out of host memory");
-  plan->info.kind = REDSET_HIP_PLAN_XOR_REBUILD;
-  plan->info.ranks = ranks;
-  plan->info.encoding = 1;
-  plan->info.missing = 1;
-  plan->info.chunk_size = chunk_size;
-  if (int rc = build_xor_plan(plan, stripes, chunk_size)) {
-    redset_hip_plan_destroy(plan);
-    return rc;
-  }
-  *out = plan;
-  return REDSET_SUCCESS;
+  std::vector<StripeMap> maps(ranks);
+  for (int c = 0; c < ranks; ++c) redset_hip::xor_rebuild_map(ranks, root, c, maps[c]);
+  return finish_plan(REDSET_HIP_PLAN_XOR_REBUILD, ranks, 1, 1, chunk_size, maps, SetLayout{lofi, xorc, stride}, out);
 }
 
 int redset_hip_plan_execute(const redset_hip_plan* plan, void* stream) {
   if (!plan) return fail("null plan");
-  for (const GfLaunch& L : plan->gf_launches)
-    if (int e = redset_hip::launch_gf(L, stream))
-      return hip_check(static_cast<hipError_t>(e), "gf_mac launch");
-  for (const XorLaunch& L : plan->xor_launches)
-    if (int e = redset_hip::launch_xor(L, stream))
-      return hip_check(static_cast<hipError_t>(e), "xor launch");
+  for (const GfLaunch& G : plan->gf_launches)
+    if (int e = redset_hip::launch_gf(G, stream)) return hip_check(static_cast<hipError_t>(e), "gf_mac launch");
+  for (const XorLaunch& X : plan->xor_launches)
+    if (int e = redset_hip::launch_xor(X, stream)) return hip_check(static_cast<hipError_t>(e), "xor launch");
   return REDSET_SUCCESS;
 }
 
@@ -540,16 +436,16 @@ int redset_hip_gf_combine(const unsigned char* const* in, int nin, unsigned char
     al = al && aligned16(out[j]);
     for (int i = 0; i < nin; ++i) J.coef[j][i] = coeffs[j * nin + i];
   }
-  GfLaunch L;
-  std::memset(&L, 0, sizeof(L));
-  L.njobs = 1;
-  L.nin = nin;
-  L.nout = nout;
-  L.accumulate = accumulate ? 1 : 0;
-  L.bytes_only = al ? 0 : 1;
-  L.nbytes = nbytes;
-  L.blocks_per_job = blocks_per_job(1, nbytes, redset_hip::gf_blocks_per_cu(nin));
-  return hip_check(static_cast<hipError_t>(redset_hip::launch_gf_single(L, J, stream)), "gf_combine launch");
+  GfLaunch G;
+  std::memset(&G, 0, sizeof(G));
+  G.njobs = 1;
+  G.nin = nin;
+  G.nout = nout;
+  G.accumulate = accumulate ? 1 : 0;
+  G.bytes_only = al ? 0 : 1;
+  G.nbytes = nbytes;
+  G.blocks_per_job = blocks_per_job(1, nbytes, redset_hip::gf_blocks_per_cu(nin));
+  return hip_check(static_cast<hipError_t>(redset_hip::launch_gf_single(G, J, stream)), "gf_combine launch");
 }
 
 int redset_hip_xor_combine(const unsigned char* const* in, int nin, unsigned char* out, size_t nbytes, int accumulate,
@@ -565,15 +461,15 @@ int redset_hip_xor_combine(const unsigned char* const* in, int nin, unsigned cha
     al = al && aligned16(in[i]);
   }
   J.out = out;
-  XorLaunch L;
-  std::memset(&L, 0, sizeof(L));
-  L.njobs = 1;
-  L.nin = nin;
-  L.accumulate = accumulate ? 1 : 0;
-  L.bytes_only = al ? 0 : 1;
-  L.nbytes = nbytes;
-  L.blocks_per_job = blocks_per_job(1, nbytes, 8);
-  return hip_check(static_cast<hipError_t>(redset_hip::launch_xor_single(L, J, stream)), "xor_combine launch");
+  XorLaunch X;
+  std::memset(&X, 0, sizeof(X));
+  X.njobs = 1;
+  X.nin = nin;
+  X.accumulate = accumulate ? 1 : 0;
+  X.bytes_only = al ? 0 : 1;
+  X.nbytes = nbytes;
+  X.blocks_per_job = blocks_per_job(1, nbytes, 8);
+  return hip_check(static_cast<hipError_t>(redset_hip::launch_xor_single(X, J, stream)), "xor_combine launch");
 }
 
 }  // extern "C"

@@ -1,0 +1,556 @@
+// stream_pipeline.cpp -- host-resident encode / rebuild through pinned
+// staging buffers and HBM (include/redset_hip.h, "streaming pipeline").
+//
+// The reference runs its codec slice by slice: read a 1 MiB slice of each
+// input (redset_lofi_pread), combine, write the parity slice after the
+// header (src/redset_reedsolomon.c:309-391, src/redset_reedsolomon_serial.c:
+// 226-325). Here a (stripe, slice) *unit* flows through four overlapped
+// stages on NSLOT rotating slots:
+//   read    I/O threads fill the slot's pinned input buffer (io->read)
+//   H2D     hipMemcpyAsync on the copy-in stream
+//   compute gf_mac / xor kernel on the compute stream (run_stripe)
+//   D2H     hipMemcpyAsync on the copy-out stream, then I/O threads drain
+//           the pinned output buffer (io->write)
+// so PCIe in, PCIe out, the kernel and host I/O of different units run at
+// the same time. A slot returns to the reader only after its writes finish.
+#include <fcntl.h>
+#include <hip/hip_runtime.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <chrono>
+#include <condition_variable>
+#include <cstring>
+#include <functional>
+#include <mutex>
+#include <new>
+#include <queue>
+#include <string>
+#include <thread>
+#include <vector>
+
+#include "redset_hip.h"
+#include "stripe_map.h"
+
+using redset_hip::CellRef;
+using redset_hip::fail;
+using redset_hip::StripeMap;
+
+namespace {
+
+double now_s() {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Fixed pool of I/O workers; run() executes a batch and waits for it.
+class IoPool {
+ public:
+  explicit IoPool(int n) {
+    for (int i = 0; i < n; ++i) workers_.emplace_back([this] { loop(); });
+  }
+  ~IoPool() {
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      quit_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : workers_) t.join();
+  }
+  // run every task, return when all are done
+  void run(std::vector<std::function<void()>>& tasks) {
+    std::atomic<int> left(static_cast<int>(tasks.size()));
+    std::mutex dmu;
+    std::condition_variable dcv;
+    {
+      std::lock_guard<std::mutex> g(mu_);
+      for (auto& t : tasks) {
+        q_.push([&t, &left, &dmu, &dcv] {
+          t();
+          if (left.fetch_sub(1) == 1) {
+            std::lock_guard<std::mutex> g2(dmu);
+            dcv.notify_all();
+          }
+        });
+      }
+    }
+    cv_.notify_all();
+    std::unique_lock<std::mutex> lk(dmu);
+    dcv.wait(lk, [&] { return left.load() == 0; });
+  }
+
+ private:
+  void loop() {
+    for (;;) {
+      std::function<void()> f;
+      {
+        std::unique_lock<std::mutex> lk(mu_);
+        cv_.wait(lk, [this] { return quit_ || !q_.empty(); });
+        if (quit_ && q_.empty()) return;
+        f = std::move(q_.front());
+        q_.pop();
+      }
+      f();
+    }
+  }
+  std::vector<std::thread> workers_;
+  std::queue<std::function<void()>> q_;
+  std::mutex mu_;
+  std::condition_variable cv_;
+  bool quit_ = false;
+};
+
+struct Unit {
+  int map;      // index into maps
+  size_t off;   // byte offset within each cell
+  size_t len;
+};
+
+enum SlotState { kFree, kRead, kOnGpu };
+
+struct Slot {
+  uint8_t* h_in = nullptr;
+  uint8_t* h_out = nullptr;
+  uint8_t* d_in = nullptr;
+  uint8_t* d_out = nullptr;
+  hipEvent_t ev_in = nullptr, ev_comp = nullptr, ev_done = nullptr, ev_start = nullptr;
+  SlotState state = kFree;
+  size_t unit = 0;
+};
+
+constexpr int kSlots = 4;
+
+int hip_ok(hipError_t e, const char* what) { return e == hipSuccess ? 0 : fail("%s: %s", what, hipGetErrorString(e)); }
+
+int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice, int io_threads,
+                 const redset_hip_io* io, redset_hip_stream_stats* stats) {
+  if (!io || !io->read || !io->write) return fail("null redset_hip_io");
+  if (slice == 0) slice = 8u << 20;
+  slice = std::min(slice, std::max<size_t>(chunk, 1));
+  slice = (slice + 255) & ~static_cast<size_t>(255);
+  if (io_threads <= 0) io_threads = 8;
+  const double t0 = now_s();
+  size_t max_in = 0, max_out = 0;
+  for (const StripeMap& m : maps) {
+    max_in = std::max(max_in, m.in.size());
+    max_out = std::max(max_out, m.out.size());
+  }
+  std::vector<Unit> units;
+  for (size_t k = 0; k < maps.size(); ++k)
+    for (size_t off = 0; off < chunk; off += slice) units.push_back(Unit{static_cast<int>(k), off, std::min(slice, chunk - off)});
+  redset_hip_stream_stats st;
+  std::memset(&st, 0, sizeof(st));
+  if (units.empty() || max_out == 0) {
+    if (stats) *stats = st;
+    return REDSET_SUCCESS;
+  }
+
+  Slot slots[kSlots];
+  hipStream_t s_in = nullptr, s_comp = nullptr, s_out = nullptr;
+  int rc = 0;
+  rc = rc ? rc : hip_ok(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking), "stream");
+  rc = rc ? rc : hip_ok(hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking), "stream");
+  rc = rc ? rc : hip_ok(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking), "stream");
+  for (Slot& S : slots) {
+    rc = rc ? rc : hip_ok(hipHostMalloc(reinterpret_cast<void**>(&S.h_in), max_in * slice, hipHostMallocDefault), "hipHostMalloc");
+    rc = rc ? rc : hip_ok(hipHostMalloc(reinterpret_cast<void**>(&S.h_out), max_out * slice, hipHostMallocDefault), "hipHostMalloc");
+    rc = rc ? rc : hip_ok(hipMalloc(reinterpret_cast<void**>(&S.d_in), max_in * slice), "hipMalloc");
+    rc = rc ? rc : hip_ok(hipMalloc(reinterpret_cast<void**>(&S.d_out), max_out * slice), "hipMalloc");
+    rc = rc ? rc : hip_ok(hipEventCreateWithFlags(&S.ev_in, hipEventDisableTiming), "event");
+    rc = rc ? rc : hip_ok(hipEventCreateWithFlags(&S.ev_comp, hipEventDisableTiming), "event");
+    rc = rc ? rc : hip_ok(hipEventCreate(&S.ev_start), "event");
+    rc = rc ? rc : hip_ok(hipEventCreate(&S.ev_done), "event");
+  }
+
+  std::mutex mu;
+  std::condition_variable cv;
+  std::atomic<int> io_err(0);
+  std::atomic<long long> read_ns(0), write_ns(0);
+  double gpu_s = 0;
+  const size_t nunits = units.size();
+
+  if (rc == 0) {
+    IoPool rpool(io_threads), wpool(std::max(1, io_threads / 2));
+
+    std::atomic<bool> abort(false);
+    // false if the pipeline was aborted while waiting
+    auto wait_state = [&](Slot& S, SlotState want) {
+      std::unique_lock<std::mutex> lk(mu);
+      cv.wait(lk, [&] { return S.state == want || abort.load(); });
+      return !abort.load();
+    };
+    auto set_state = [&](Slot& S, SlotState s) {
+      {
+        std::lock_guard<std::mutex> g(mu);
+        S.state = s;
+      }
+      cv.notify_all();
+    };
+
+    // reader: fills slots ahead of the GPU
+    std::thread reader([&] {
+      for (size_t u = 0; u < nunits; ++u) {
+        Slot& S = slots[u % kSlots];
+        if (!wait_state(S, kFree)) return;
+        const Unit& U = units[u];
+        const StripeMap& m = maps[U.map];
+        std::vector<std::function<void()>> tasks;
+        for (size_t i = 0; i < m.in.size(); ++i) {
+          tasks.push_back([&, i, U] {
+            const CellRef& c = maps[U.map].in[i];
+            const double a = now_s();
+            if (io->read(io->ctx, c.rank, c.kind, c.index, U.off, U.len, S.h_in + i * slice) != 0) io_err = 1;
+            read_ns += static_cast<long long>((now_s() - a) * 1e9);
+          });
+        }
+        rpool.run(tasks);
+        S.unit = u;
+        set_state(S, kRead);
+      }
+    });
+
+    // writer: drains slots after D2H
+    std::thread writer([&] {
+      for (size_t u = 0; u < nunits; ++u) {
+        Slot& S = slots[u % kSlots];
+        if (!wait_state(S, kOnGpu)) return;
+        if (hipEventSynchronize(S.ev_done) != hipSuccess) io_err = 2;
+        float ms = 0;
+        if (hipEventElapsedTime(&ms, S.ev_start, S.ev_done) == hipSuccess) gpu_s += ms * 1e-3;
+        const Unit& U = units[u];
+        const StripeMap& m = maps[U.map];
+        std::vector<std::function<void()>> tasks;
+        for (size_t j = 0; j < m.out.size(); ++j) {
+          tasks.push_back([&, j, U] {
+            const CellRef& c = maps[U.map].out[j];
+            const double a = now_s();
+            if (io->write(io->ctx, c.rank, c.kind, c.index, U.off, U.len, S.h_out + j * slice) != 0) io_err = 1;
+            write_ns += static_cast<long long>((now_s() - a) * 1e9);
+          });
+        }
+        wpool.run(tasks);
+        set_state(S, kFree);
+      }
+    });
+
+    // GPU feeder (this thread)
+    std::vector<const uint8_t*> ins;
+    std::vector<uint8_t*> outs;
+    for (size_t u = 0; u < nunits && rc == 0; ++u) {
+      Slot& S = slots[u % kSlots];
+      if (!wait_state(S, kRead)) break;
+      const Unit& U = units[u];
+      const StripeMap& m = maps[U.map];
+      const size_t nin = m.in.size(), nout = m.out.size();
+      rc = rc ? rc : hip_ok(hipEventRecord(S.ev_start, s_in), "event record");
+      for (size_t i = 0; i < nin && rc == 0; ++i)
+        rc = hip_ok(hipMemcpyAsync(S.d_in + i * slice, S.h_in + i * slice, U.len, hipMemcpyHostToDevice, s_in), "H2D");
+      rc = rc ? rc : hip_ok(hipEventRecord(S.ev_in, s_in), "event record");
+      rc = rc ? rc : hip_ok(hipStreamWaitEvent(s_comp, S.ev_in, 0), "stream wait");
+      ins.resize(nin);
+      outs.resize(nout);
+      for (size_t i = 0; i < nin; ++i) ins[i] = S.d_in + i * slice;
+      for (size_t j = 0; j < nout; ++j) outs[j] = S.d_out + j * slice;
+      if (rc == 0) rc = redset_hip::run_stripe(m, ins.data(), outs.data(), U.len, s_comp, 0);
+      rc = rc ? rc : hip_ok(hipEventRecord(S.ev_comp, s_comp), "event record");
+      rc = rc ? rc : hip_ok(hipStreamWaitEvent(s_out, S.ev_comp, 0), "stream wait");
+      for (size_t j = 0; j < nout && rc == 0; ++j)
+        rc = hip_ok(hipMemcpyAsync(S.h_out + j * slice, S.d_out + j * slice, U.len, hipMemcpyDeviceToHost, s_out), "D2H");
+      rc = rc ? rc : hip_ok(hipEventRecord(S.ev_done, s_out), "event record");
+      st.bytes_read += nin * U.len;
+      st.bytes_written += nout * U.len;
+      st.units += 1;
+      set_state(S, kOnGpu);
+    }
+    if (rc != 0) {
+      // a HIP failure: stop the reader and writer wherever they wait
+      {
+        std::lock_guard<std::mutex> g(mu);
+        abort = true;
+      }
+      cv.notify_all();
+    }
+    reader.join();
+    writer.join();
+  }
+  (void) hipStreamSynchronize(s_in);
+  (void) hipStreamSynchronize(s_comp);
+  (void) hipStreamSynchronize(s_out);
+  for (Slot& S : slots) {
+    if (S.h_in) (void) hipHostFree(S.h_in);
+    if (S.h_out) (void) hipHostFree(S.h_out);
+    if (S.d_in) (void) hipFree(S.d_in);
+    if (S.d_out) (void) hipFree(S.d_out);
+    if (S.ev_in) (void) hipEventDestroy(S.ev_in);
+    if (S.ev_comp) (void) hipEventDestroy(S.ev_comp);
+    if (S.ev_start) (void) hipEventDestroy(S.ev_start);
+    if (S.ev_done) (void) hipEventDestroy(S.ev_done);
+  }
+  if (s_in) (void) hipStreamDestroy(s_in);
+  if (s_comp) (void) hipStreamDestroy(s_comp);
+  if (s_out) (void) hipStreamDestroy(s_out);
+  st.seconds = now_s() - t0;
+  st.read_seconds = read_ns.load() * 1e-9;
+  st.write_seconds = write_ns.load() * 1e-9;
+  st.gpu_seconds = gpu_s;
+  if (stats) *stats = st;
+  if (rc) return rc;
+  if (io_err.load()) return fail("stream I/O callback failed");
+  return REDSET_SUCCESS;
+}
+
+int stripe_range(int ranks, int first, int n, int& lo, int& hi) {
+  if (n <= 0) {
+    first = 0;
+    n = ranks;
+  }
+  if (first < 0 || first + n > ranks) return fail("stripe range [%d, %d) outside 0..%d", first, first + n, ranks);
+  lo = first;
+  hi = first + n;
+  return 0;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// built-in I/O: host memory
+// ---------------------------------------------------------------------------
+
+struct redset_hip_hostio {
+  std::vector<unsigned char*> lofi, parity;
+  size_t stride;
+};
+
+namespace {
+int hostio_read(void* ctx, int rank, int kind, int index, unsigned long long off, size_t len, void* dst) {
+  auto* h = static_cast<redset_hip_hostio*>(ctx);
+  const unsigned char* base = kind == REDSET_HIP_CELL_DATA ? h->lofi[rank] : h->parity[rank];
+  std::memcpy(dst, base + static_cast<size_t>(index) * h->stride + off, len);
+  return 0;
+}
+int hostio_write(void* ctx, int rank, int kind, int index, unsigned long long off, size_t len, const void* src) {
+  auto* h = static_cast<redset_hip_hostio*>(ctx);
+  unsigned char* base = kind == REDSET_HIP_CELL_DATA ? h->lofi[rank] : h->parity[rank];
+  std::memcpy(base + static_cast<size_t>(index) * h->stride + off, src, len);
+  return 0;
+}
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// built-in I/O: files with redset logical-file semantics
+// ---------------------------------------------------------------------------
+
+struct redset_hip_fileio {
+  struct File {
+    std::string path;
+    unsigned long long size;
+    int fd;
+    bool writable;
+  };
+  std::vector<std::vector<File>> data;  // member -> its files, in logical order
+  std::vector<int> red_fd;
+  std::vector<unsigned long long> header;
+  size_t chunk;
+};
+
+namespace {
+
+// pread/pwrite of a full range, retrying short transfers and EINTR
+// (redset_read_attempt / redset_write_attempt, src/redset_io.c:234-310)
+int full_pread(int fd, void* buf, size_t len, off_t off) {
+  char* p = static_cast<char*>(buf);
+  while (len > 0) {
+    ssize_t n = ::pread(fd, p, len, off);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      return -1;
+    }
+    if (n == 0) {  // EOF: zero fill (logical file padding)
+      std::memset(p, 0, len);
+      return 0;
+    }
+    p += n;
+    len -= static_cast<size_t>(n);
+    off += n;
+  }
+  return 0;
+}
+
+int full_pwrite(int fd, const void* buf, size_t len, off_t off) {
+  const char* p = static_cast<const char*>(buf);
+  while (len > 0) {
+    ssize_t n = ::pwrite(fd, p, len, off);
+    if (n < 0) {
+      if (errno == EINTR) continue;
+      return -1;
+    }
+    p += n;
+    len -= static_cast<size_t>(n);
+    off += n;
+  }
+  return 0;
+}
+
+// redset_read_pad_n / redset_write_pad_n (src/redset_lofi.c:30-173): walk the
+// member's files over the logical range [pos, pos+len)
+int lofi_rw(redset_hip_fileio* f, int rank, unsigned long long pos, size_t len, char* buf, bool write) {
+  unsigned long long start = 0;
+  for (const auto& F : f->data[rank]) {
+    const unsigned long long end = start + F.size;
+    if (pos < end && len > 0) {
+      const size_t n = static_cast<size_t>(std::min<unsigned long long>(len, end - pos));
+      const off_t off = static_cast<off_t>(pos - start);
+      const int r = write ? full_pwrite(F.fd, buf, n, off) : full_pread(F.fd, buf, n, off);
+      if (r != 0) return -1;
+      pos += n;
+      buf += n;
+      len -= n;
+    }
+    start = end;
+  }
+  if (len > 0 && !write) std::memset(buf, 0, len);  // past the last file: zeros
+  return 0;
+}
+
+int fileio_read(void* ctx, int rank, int kind, int index, unsigned long long off, size_t len, void* dst) {
+  auto* f = static_cast<redset_hip_fileio*>(ctx);
+  if (kind == REDSET_HIP_CELL_DATA)
+    return lofi_rw(f, rank, static_cast<unsigned long long>(index) * f->chunk + off, len, static_cast<char*>(dst), false);
+  return full_pread(f->red_fd[rank], dst, len, static_cast<off_t>(f->header[rank] + index * f->chunk + off));
+}
+
+int fileio_write(void* ctx, int rank, int kind, int index, unsigned long long off, size_t len, const void* src) {
+  auto* f = static_cast<redset_hip_fileio*>(ctx);
+  if (kind == REDSET_HIP_CELL_DATA)
+    return lofi_rw(f, rank, static_cast<unsigned long long>(index) * f->chunk + off, len,
+                   const_cast<char*>(static_cast<const char*>(src)), true);
+  return full_pwrite(f->red_fd[rank], src, len, static_cast<off_t>(f->header[rank] + index * f->chunk + off));
+}
+
+}  // namespace
+
+extern "C" {
+
+int redset_hip_rs_encode_stream(const redset_hip_rs* rs, size_t chunk_size, int first_stripe, int nstripes,
+                                size_t slice_bytes, int io_threads, const redset_hip_io* io,
+                                redset_hip_stream_stats* stats) {
+  if (!rs) return fail("null rs state");
+  int lo, hi;
+  if (int rc = stripe_range(rs->ranks, first_stripe, nstripes, lo, hi)) return rc;
+  std::vector<StripeMap> maps(hi - lo);
+  for (int c = lo; c < hi; ++c) redset_hip::rs_encode_map(rs, c, maps[c - lo]);
+  return run_pipeline(maps, chunk_size, slice_bytes, io_threads, io, stats);
+}
+
+int redset_hip_rs_rebuild_stream(const redset_hip_rs* rs, int missing, const int* rebuild_ranks, size_t chunk_size,
+                                 int first_stripe, int nstripes, size_t slice_bytes, int io_threads,
+                                 const redset_hip_io* io, redset_hip_stream_stats* stats) {
+  if (!rs || !rebuild_ranks) return fail("null argument");
+  int lo, hi;
+  if (int rc = stripe_range(rs->ranks, first_stripe, nstripes, lo, hi)) return rc;
+  std::vector<StripeMap> maps(hi - lo);
+  for (int c = lo; c < hi; ++c)
+    if (int rc = redset_hip::rs_rebuild_map(rs, missing, rebuild_ranks, c, maps[c - lo])) return rc;
+  return run_pipeline(maps, chunk_size, slice_bytes, io_threads, io, stats);
+}
+
+int redset_hip_xor_encode_stream(int ranks, size_t chunk_size, int first_stripe, int nstripes, size_t slice_bytes,
+                                 int io_threads, const redset_hip_io* io, redset_hip_stream_stats* stats) {
+  if (ranks < 2) return fail("XOR needs at least 2 ranks, got %d", ranks);
+  int lo, hi;
+  if (int rc = stripe_range(ranks, first_stripe, nstripes, lo, hi)) return rc;
+  std::vector<StripeMap> maps(hi - lo);
+  for (int c = lo; c < hi; ++c) redset_hip::xor_encode_map(ranks, c, maps[c - lo]);
+  return run_pipeline(maps, chunk_size, slice_bytes, io_threads, io, stats);
+}
+
+int redset_hip_xor_rebuild_stream(int ranks, int root, size_t chunk_size, int first_stripe, int nstripes,
+                                  size_t slice_bytes, int io_threads, const redset_hip_io* io,
+                                  redset_hip_stream_stats* stats) {
+  if (ranks < 2) return fail("XOR needs at least 2 ranks, got %d", ranks);
+  int lo, hi;
+  if (int rc = stripe_range(ranks, first_stripe, nstripes, lo, hi)) return rc;
+  std::vector<StripeMap> maps(hi - lo);
+  for (int c = lo; c < hi; ++c)
+    if (int rc = redset_hip::xor_rebuild_map(ranks, root, c, maps[c - lo])) return rc;
+  return run_pipeline(maps, chunk_size, slice_bytes, io_threads, io, stats);
+}
+
+int redset_hip_hostio_create(int ranks, unsigned char* const* lofi, unsigned char* const* parity, size_t cell_stride,
+                             redset_hip_io* io_out, redset_hip_hostio** out) {
+  if (!out || !io_out || !lofi || !parity || ranks < 1) return fail("hostio_create: bad argument");
+  auto* h = new (std::nothrow) redset_hip_hostio;
+  if (!h) return fail("out of host memory");
+  h->lofi.assign(lofi, lofi + ranks);
+  h->parity.assign(parity, parity + ranks);
+  h->stride = cell_stride;
+  io_out->read = hostio_read;
+  io_out->write = hostio_write;
+  io_out->ctx = h;
+  *out = h;
+  return REDSET_SUCCESS;
+}
+
+void redset_hip_hostio_destroy(redset_hip_hostio* h) { delete h; }
+
+int redset_hip_fileio_create(int ranks, const int* nfiles, const char* const* paths, const unsigned long long* sizes,
+                             const char* const* redundancy_paths, const unsigned long long* header_sizes,
+                             size_t chunk_size, const int* writable, redset_hip_io* io_out,
+                             redset_hip_fileio** out) {
+  if (!out || !io_out || !nfiles || !paths || !sizes || !redundancy_paths || ranks < 1)
+    return fail("fileio_create: bad argument");
+  auto* f = new (std::nothrow) redset_hip_fileio;
+  if (!f) return fail("out of host memory");
+  f->chunk = chunk_size;
+  f->data.resize(ranks);
+  f->red_fd.assign(ranks, -1);
+  f->header.assign(ranks, 0);
+  size_t k = 0;
+  int rc = 0;
+  for (int r = 0; r < ranks && rc == 0; ++r) {
+    const bool w = writable && writable[r];
+    for (int i = 0; i < nfiles[r] && rc == 0; ++i, ++k) {
+      int fd = w ? ::open(paths[k], O_RDWR | O_CREAT, 0600) : ::open(paths[k], O_RDONLY);
+      if (fd < 0) {
+        rc = fail("open(%s): %s", paths[k], strerror(errno));
+        break;
+      }
+      if (w && ::ftruncate(fd, static_cast<off_t>(sizes[k])) != 0) rc = fail("ftruncate(%s): %s", paths[k], strerror(errno));
+      f->data[r].push_back(redset_hip_fileio::File{paths[k], sizes[k], fd, w});
+    }
+    if (rc) break;
+    f->header[r] = header_sizes ? header_sizes[r] : 0;
+    f->red_fd[r] = ::open(redundancy_paths[r], O_RDWR | O_CREAT, 0600);
+    if (f->red_fd[r] < 0) rc = fail("open(%s): %s", redundancy_paths[r], strerror(errno));
+  }
+  if (rc) {
+    redset_hip_fileio_destroy(f);
+    return rc;
+  }
+  io_out->read = fileio_read;
+  io_out->write = fileio_write;
+  io_out->ctx = f;
+  *out = f;
+  return REDSET_SUCCESS;
+}
+
+void redset_hip_fileio_destroy(redset_hip_fileio* f) {
+  if (!f) return;
+  // fsync what we may have written before closing, as redset_close does
+  // (src/redset_io.c:119-139)
+  for (auto& files : f->data)
+    for (auto& F : files)
+      if (F.fd >= 0) {
+        if (F.writable) (void) ::fsync(F.fd);
+        ::close(F.fd);
+      }
+  for (int fd : f->red_fd)
+    if (fd >= 0) {
+      (void) ::fsync(fd);
+      ::close(fd);
+    }
+  delete f;
+}
+
+}  // extern "C"

@@ -1,0 +1,170 @@
+"""GPU tests of the host-resident streaming pipeline (pinned staging <-> HBM):
+host-memory and file-backed sets against the oracle, and the redset
+test_redset.c round trip (write files, encode, delete a member's files,
+rebuild, compare CRC32) through the file I/O with logical-file padding."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def rd():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import redset_amd
+    from redset_amd import stream
+
+    redset_amd.load()
+    return redset_amd, stream
+
+
+def _host_set(lofi, parity):
+    """numpy member arrays -> HostIO-compatible pointer lists (stride = chunk)"""
+    return [a.ctypes.data for a in lofi], [a.ctypes.data for a in parity]
+
+
+@pytest.mark.parametrize("p,e,chunk,slice_bytes", [(11, 3, 100_003, 16384), (20, 4, 65536, 0), (4, 2, 5000, 1024),
+                                                     (12, 6, 8192, 4096), (24, 4, 4096, 1024)])
+def test_rs_encode_stream_hostio(rd, oracle, p, e, chunk, slice_bytes):
+    redset_amd, stream = rd
+    lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=chunk + p)
+    lp, pp = _host_set(lofi, parity)
+    io = stream.HostIO(p, lp, pp, chunk, keepalive=(lofi, parity))
+    codec = redset_amd.RSCodec(p, e)
+    st = stream.rs_encode_stream(codec, chunk, io, slice_bytes=slice_bytes, io_threads=4)
+    want = [np.zeros_like(x) for x in parity]
+    oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    for r in range(p):
+        assert np.array_equal(parity[r], want[r]), r
+    assert st["bytes_written"] == p * e * chunk
+    assert st["units"] >= p
+
+
+def test_rs_encode_stream_stripe_range(rd, oracle):
+    redset_amd, stream = rd
+    p, e, chunk = 11, 3, 40000
+    lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=1)
+    io = stream.HostIO(p, *_host_set(lofi, parity), chunk, keepalive=(lofi, parity))
+    st = stream.rs_encode_stream(redset_amd.RSCodec(p, e), chunk, io, first=3, nstripes=2)
+    want = [np.zeros_like(x) for x in parity]
+    oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    # only the parity cells of stripes 3 and 4 are written
+    for r in range(p):
+        for i in range(e):
+            c = (r + i) % p
+            got = parity[r][i * chunk:(i + 1) * chunk]
+            if c in (3, 4):
+                assert np.array_equal(got, want[r][i * chunk:(i + 1) * chunk])
+            else:
+                assert not got.any()
+    assert st["bytes_read"] == 2 * (p - e) * chunk
+
+
+@pytest.mark.parametrize("p,e,lost", [(11, 3, [1, 2]), (11, 3, [0, 5, 10]), (20, 4, [3, 4, 17, 19]), (6, 3, [5])])
+def test_rs_rebuild_stream_hostio(rd, oracle, p, e, lost):
+    redset_amd, stream = rd
+    chunk = 30001
+    lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=p * 7)
+    oracle.OracleRS(p, e).encode_set(lofi, parity, chunk)
+    ref_l = [x.copy() for x in lofi]
+    ref_p = [x.copy() for x in parity]
+    for r in lost:
+        lofi[r][:] = 0
+        parity[r][:] = 0
+    io = stream.HostIO(p, *_host_set(lofi, parity), chunk, keepalive=(lofi, parity))
+    stream.rs_rebuild_stream(redset_amd.RSCodec(p, e), lost, chunk, io, slice_bytes=8192)
+    for r in range(p):
+        assert np.array_equal(lofi[r], ref_l[r]) and np.array_equal(parity[r], ref_p[r]), r
+
+
+def test_xor_stream_hostio(rd, oracle):
+    redset_amd, stream = rd
+    p, chunk = 8, 70001
+    lofi, xorc = oracle.random_set(p, p - 1, 1, chunk, seed=4)
+    io = stream.HostIO(p, *_host_set(lofi, xorc), chunk, keepalive=(lofi, xorc))
+    stream.xor_encode_stream(p, chunk, io, slice_bytes=16384)
+    want = [np.zeros_like(x) for x in xorc]
+    oracle.xor_encode_set(p, lofi, want, chunk)
+    assert all(np.array_equal(a, b) for a, b in zip(xorc, want))
+    ref = lofi[6].copy()
+    lofi[6][:] = 0
+    xorc[6][:] = 0
+    stream.xor_rebuild_stream(p, 6, chunk, io)
+    assert np.array_equal(lofi[6], ref) and np.array_equal(xorc[6], want[6])
+
+
+def _write_member_files(tmp, r, rng, nfiles, maxsize):
+    files = []
+    for k in range(nfiles):
+        size = int(rng.integers(0, maxsize))
+        path = os.path.join(tmp, f"rank{r}_file{k}.dat")
+        data = rng.integers(0, 256, size, dtype=np.uint8)
+        data.tofile(path)
+        files.append((path, size))
+    return files
+
+
+def _logical(files, total):
+    """redset logical file: concatenation zero-padded to `total` bytes"""
+    parts = [np.fromfile(p, dtype=np.uint8) for p, _ in files]
+    cat = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    out = np.zeros(total, np.uint8)
+    out[:cat.size] = cat
+    return out
+
+
+@pytest.mark.parametrize("scheme", ["rs", "xor"])
+def test_file_round_trip_crc(rd, oracle, tmp_path, scheme):
+    """test/test_redset.c semantics: each rank writes files, apply, delete a
+    rank's files, recover, check CRC32 of every rebuilt file
+    (test_redset.c:459-589), here for a whole set in one process."""
+    redset_amd, stream = rd
+    rng = np.random.default_rng(11)
+    p, e = (8, 3) if scheme == "rs" else (4, 1)
+    d = p - e
+    tmp = str(tmp_path)
+    files = [_write_member_files(tmp, r, rng, nfiles=int(rng.integers(1, 4)), maxsize=300_000) for r in range(p)]
+    max_bytes = max(sum(s for _, s in f) for f in files)
+    chunk = stream.chunk_size_for(max_bytes, d)
+    header = [4096 + 13 * r for r in range(p)]  # stands in for the kvtree header
+    reds = [os.path.join(tmp, f"rank{r}.{scheme}.redset") for r in range(p)]
+    crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for f in files for path, _ in f}
+    io = stream.FileIO(files, reds, header, chunk)
+    if scheme == "rs":
+        codec = redset_amd.RSCodec(p, e)
+        stream.rs_encode_stream(codec, chunk, io, slice_bytes=65536)
+    else:
+        stream.xor_encode_stream(p, chunk, io, slice_bytes=65536)
+    io.close()
+    # parity bytes after the header equal the oracle's on the padded logical files
+    lofi = [_logical(f, d * chunk) for f in files]
+    want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+    if scheme == "rs":
+        oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    else:
+        oracle.xor_encode_set(p, lofi, want, chunk)
+    for r in range(p):
+        got = np.fromfile(reds[r], dtype=np.uint8)[header[r]:header[r] + e * chunk]
+        assert np.array_equal(got, want[r]), r
+    # lose members (files and redundancy file), rebuild, check CRC32
+    lost = [1, 6] if scheme == "rs" else [2]
+    for r in lost:
+        for path, _ in files[r]:
+            os.unlink(path)
+        os.unlink(reds[r])
+    io = stream.FileIO(files, reds, header, chunk, writable=[r in lost for r in range(p)])
+    if scheme == "rs":
+        stream.rs_rebuild_stream(codec, lost, chunk, io, slice_bytes=32768)
+    else:
+        stream.xor_rebuild_stream(p, lost[0], chunk, io, slice_bytes=32768)
+    io.close()
+    for r in lost:
+        for path, size in files[r]:
+            assert os.path.getsize(path) == size
+            assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
+        got = np.fromfile(reds[r], dtype=np.uint8)[header[r]:header[r] + e * chunk]
+        assert np.array_equal(got, want[r]), r

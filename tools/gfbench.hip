@@ -86,6 +86,7 @@ __device__ __forceinline__ void st(uint4* p, uint4 v) {
   }
 }
 
+__constant__ int g_skew;
 template <int NIN, int MODE, bool NT, int U, int BLOCK, bool GS = false>
 __global__ void __launch_bounds__(BLOCK) kvar(const Job* jobs, size_t nvec, int bpj, int nout) {
   __shared__ uint32_t lds[MODE == FULLTAB ? NIN * 256 : NIN * 32];
@@ -123,7 +124,11 @@ __global__ void __launch_bounds__(BLOCK) kvar(const Job* jobs, size_t nvec, int 
 #pragma unroll
   for (int j = 0; j < kMaxOut; ++j) out[j] = reinterpret_cast<uint4*>(J.out[j]);
 
-  for (size_t vb = v0 + threadIdx.x; vb < v1; vb += vstep) {
+  // skew: job j starts its sweep j/njobs of the way into the cells (wraps)
+  const size_t shift = g_skew ? (nvec / gridDim.x * bpj) * job : 0;
+  for (size_t vb0 = v0 + threadIdx.x; vb0 < v1; vb0 += vstep) {
+    size_t vb = vb0 + shift;
+    if (vb >= nvec) vb -= nvec;
     uint4 x[U][NIN];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -134,6 +139,7 @@ __global__ void __launch_bounds__(BLOCK) kvar(const Job* jobs, size_t nvec, int 
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const size_t v = vb + (size_t)u * BLOCK;
+      (void)v1;
       uint32_t acc[16];
 #pragma unroll
       for (int b = 0; b < 16; ++b) acc[b] = 0;
@@ -394,14 +400,20 @@ float run_pipe(const Setup& S, int blocks_per_cu, int cus, int reps, double byte
 
 int main(int argc, char** argv) {
   const size_t C = (argc > 1 ? atol(argv[1]) : 64) << 20;
+  const size_t pad = argc > 2 ? atol(argv[2]) : 0;        // bytes between consecutive cells
+  const int skew = argc > 3 ? atoi(argv[3]) : 0;          // 1: jobs start their sweep at staggered offsets
   const int stripes = 11, nin = 8, nout = 3;
   hipDeviceProp_t prop;
   CHECK(hipGetDeviceProperties(&prop, 0));
   const int cus = prop.multiProcessorCount;
   printf("device %s, %d CUs, chunk %zu MiB\n", prop.name, cus, C >> 20);
-  const size_t total = (size_t)stripes * (nin + nout) * C;
+  const size_t cstride = C + pad;
+  const size_t total = (size_t)stripes * (nin + nout) * cstride;
+  const int nalloc = argc > 4 ? atoi(argv[4]) : 1;
+  for (int alloc = 0; alloc < nalloc; ++alloc) {
   uint8_t* buf;
   CHECK(hipMalloc(&buf, total));
+  printf("== allocation %d at %p\n", alloc, (void*)buf);
   // random fill via a simple LCG kernel substitute: memset pattern then host init of a few MB is enough?
   {
     std::vector<uint8_t> h(64 << 20);
@@ -419,20 +431,22 @@ int main(int argc, char** argv) {
   for (int c = 0; c < stripes; ++c) {
     Job J;
     memset(&J, 0, sizeof(J));
-    uint8_t* base = buf + (size_t)c * (nin + nout) * C;
-    for (int i = 0; i < nin; ++i) J.in[i] = base + (size_t)i * C;
-    for (int j = 0; j < nout; ++j) J.out[j] = base + (size_t)(nin + j) * C;
+    uint8_t* base = buf + (size_t)c * (nin + nout) * cstride;
+    for (int i = 0; i < nin; ++i) J.in[i] = base + (size_t)i * cstride;
+    for (int j = 0; j < nout; ++j) J.out[j] = base + (size_t)(nin + j) * cstride;
     for (int j = 0; j < nout; ++j)
       for (int i = 0; i < nin; ++i) J.coef[j][i] = (uint8_t)(17 * j + 29 * i + 3);
     S.jobs.push_back(J);
   }
   CHECK(hipMalloc(&S.d_jobs, S.jobs.size() * sizeof(Job)));
   CHECK(hipMemcpy(S.d_jobs, S.jobs.data(), S.jobs.size() * sizeof(Job), hipMemcpyHostToDevice));
-  const double bytes = (double)total;
+  const double bytes = (double)stripes * (nin + nout) * C;
+  CHECK(hipMemcpyToSymbol(HIP_SYMBOL(g_skew), &skew, sizeof(int)));
+  printf("cell pad %zu B, skew %d\n", pad, skew);
   const int reps = 10;
 
   // ceilings
-  {
+  if (getenv("GFBENCH_COPY")) {
     hipEvent_t a, b;
     CHECK(hipEventCreate(&a));
     CHECK(hipEventCreate(&b));
@@ -451,17 +465,10 @@ int main(int argc, char** argv) {
       printf("%-44s grid=%d  %8.4f ms  %8.1f GB/s\n", "copy (1 in -> 1 out, float4)", g, ms, (double)total / (ms * 1e-3) / 1e9);
     }
   }
-  for (int round = 0; round < 2; ++round) {
-    printf("-- round %d\n", round);
-    run<8, MEMONLY, false, 1, 256, true>(S, 4, cus, reps, "memonly GS", bytes);
-    run<8, MEMONLY, false, 1, 256, true>(S, 3, cus, reps, "memonly GS", bytes);
-    run<8, PROD, false, 1, 256, true>(S, 2, cus, reps, "prod GS", bytes);
-    run<8, PROD, false, 1, 256, true>(S, 3, cus, reps, "prod GS", bytes);
-    run<8, PROD, false, 1, 256, true>(S, 4, cus, reps, "prod GS", bytes);
-    run<8, PROD, false, 1, 256, true>(S, 6, cus, reps, "prod GS", bytes);
-    for (int bpc : {2, 3, 4}) run_pipe(S, bpc, cus, reps, bytes);
-    run<8, PROD, false, 1, 512, true>(S, 2, cus, reps, "prod GS", bytes);
-    run<8, PROD, false, 1, 1024, true>(S, 1, cus, reps, "prod GS", bytes);
+  {
+    run<8, MEMONLY, false, 1, 256, true>(S, 2, cus, reps, "memonly GS", bytes);
+    run_pipe(S, 4, cus, reps, bytes);
   }
+  }  // allocations (kept live so each one gets new physical pages)
   return 0;
 }

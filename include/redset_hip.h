@@ -156,6 +156,10 @@ typedef struct {
    * success. Called concurrently from the pipeline's I/O threads. */
   int (*read)(void* ctx, int rank, int kind, int index, unsigned long long offset, size_t len, void* dst);
   int (*write)(void* ctx, int rank, int kind, int index, unsigned long long offset, size_t len, const void* src);
+  /* Optional (may be NULL): host address of the cell bytes at `offset` if
+   * that memory is page-locked, so the pipeline can DMA it directly instead
+   * of staging it through read/write; NULL = use read/write. */
+  void* (*map)(void* ctx, int rank, int kind, int index, unsigned long long offset);
   void* ctx;
 } redset_hip_io;
 
@@ -184,10 +188,12 @@ int redset_hip_xor_rebuild_stream(int ranks, int root, size_t chunk_size, int fi
                                   redset_hip_stream_stats* stats);
 
 /* Built-in I/O over host memory laid out like the device set layout
- * (lofi[r] + s*cell_stride, parity[r] + i*cell_stride). */
+ * (lofi[r] + s*cell_stride, parity[r] + i*cell_stride). pinned != 0 declares
+ * the memory page-locked (hipHostMalloc / hipHostRegister): cells are then
+ * DMAed directly, with no staging copy. */
 typedef struct redset_hip_hostio redset_hip_hostio;
 int redset_hip_hostio_create(int ranks, unsigned char* const* lofi, unsigned char* const* parity, size_t cell_stride,
-                             redset_hip_io* io_out, redset_hip_hostio** out);
+                             int pinned, redset_hip_io* io_out, redset_hip_hostio** out);
 void redset_hip_hostio_destroy(redset_hip_hostio* h);
 
 /* Built-in I/O over files with redset's logical-file semantics

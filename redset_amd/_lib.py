@@ -76,7 +76,7 @@ class PlanInfo(ctypes.Structure):
 class StreamIO(ctypes.Structure):
     """redset_hip_io: read/write callbacks + context (opaque here)."""
 
-    _fields_ = [("read", c_void_p), ("write", c_void_p), ("ctx", c_void_p)]
+    _fields_ = [("read", c_void_p), ("write", c_void_p), ("map", c_void_p), ("ctx", c_void_p)]
 
 
 class StreamStats(ctypes.Structure):
@@ -122,7 +122,7 @@ _SIGNATURES = {
         c_int, [c_void_p, c_int, POINTER(c_int), c_size_t, c_int, c_int, c_size_t, c_int, _IOP, _STP]),
     "redset_hip_xor_encode_stream": (c_int, [c_int, c_size_t, c_int, c_int, c_size_t, c_int, _IOP, _STP]),
     "redset_hip_xor_rebuild_stream": (c_int, [c_int, c_int, c_size_t, c_int, c_int, c_size_t, c_int, _IOP, _STP]),
-    "redset_hip_hostio_create": (c_int, [c_int, _PP, _PP, c_size_t, _IOP, POINTER(c_void_p)]),
+    "redset_hip_hostio_create": (c_int, [c_int, _PP, _PP, c_size_t, c_int, _IOP, POINTER(c_void_p)]),
     "redset_hip_hostio_destroy": (None, [c_void_p]),
     "redset_hip_fileio_create": (
         c_int,

@@ -58,9 +58,12 @@ class IoPool {
     cv_.notify_all();
     for (auto& t : workers_) t.join();
   }
-  // run every task, return when all are done
+  // run every task, return when all are done. The completion count lives
+  // under `dmu`: a worker decrements and notifies while holding it, so the
+  // caller cannot see zero, return and destroy dmu/dcv before the last
+  // worker has finished touching them.
   void run(std::vector<std::function<void()>>& tasks) {
-    std::atomic<int> left(static_cast<int>(tasks.size()));
+    int left = static_cast<int>(tasks.size());
     std::mutex dmu;
     std::condition_variable dcv;
     {
@@ -68,16 +71,14 @@ class IoPool {
       for (auto& t : tasks) {
         q_.push([&t, &left, &dmu, &dcv] {
           t();
-          if (left.fetch_sub(1) == 1) {
-            std::lock_guard<std::mutex> g2(dmu);
-            dcv.notify_all();
-          }
+          std::lock_guard<std::mutex> g2(dmu);
+          if (--left == 0) dcv.notify_all();
         });
       }
     }
     cv_.notify_all();
     std::unique_lock<std::mutex> lk(dmu);
-    dcv.wait(lk, [&] { return left.load() == 0; });
+    dcv.wait(lk, [&] { return left == 0; });
   }
 
  private:
@@ -117,6 +118,7 @@ struct Slot {
   hipEvent_t ev_in = nullptr, ev_comp = nullptr, ev_done = nullptr, ev_start = nullptr;
   SlotState state = kFree;
   size_t unit = 0;
+  std::vector<void*> src, dst;  // mapped (page-locked) host cells, or null
 };
 
 constexpr int kSlots = 4;
@@ -195,8 +197,17 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
         if (!wait_state(S, kFree)) return;
         const Unit& U = units[u];
         const StripeMap& m = maps[U.map];
+        S.src.assign(m.in.size(), nullptr);
+        S.dst.assign(m.out.size(), nullptr);
+        if (io->map) {
+          for (size_t i = 0; i < m.in.size(); ++i)
+            S.src[i] = io->map(io->ctx, m.in[i].rank, m.in[i].kind, m.in[i].index, U.off);
+          for (size_t j = 0; j < m.out.size(); ++j)
+            S.dst[j] = io->map(io->ctx, m.out[j].rank, m.out[j].kind, m.out[j].index, U.off);
+        }
         std::vector<std::function<void()>> tasks;
         for (size_t i = 0; i < m.in.size(); ++i) {
+          if (S.src[i]) continue;  // DMAed straight from mapped host memory
           tasks.push_back([&, i, U] {
             const CellRef& c = maps[U.map].in[i];
             const double a = now_s();
@@ -222,6 +233,7 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
         const StripeMap& m = maps[U.map];
         std::vector<std::function<void()>> tasks;
         for (size_t j = 0; j < m.out.size(); ++j) {
+          if (S.dst[j]) continue;  // D2H went straight to mapped host memory
           tasks.push_back([&, j, U] {
             const CellRef& c = maps[U.map].out[j];
             const double a = now_s();
@@ -244,8 +256,10 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
       const StripeMap& m = maps[U.map];
       const size_t nin = m.in.size(), nout = m.out.size();
       rc = rc ? rc : hip_ok(hipEventRecord(S.ev_start, s_in), "event record");
-      for (size_t i = 0; i < nin && rc == 0; ++i)
-        rc = hip_ok(hipMemcpyAsync(S.d_in + i * slice, S.h_in + i * slice, U.len, hipMemcpyHostToDevice, s_in), "H2D");
+      for (size_t i = 0; i < nin && rc == 0; ++i) {
+        const void* from = S.src[i] ? S.src[i] : S.h_in + i * slice;
+        rc = hip_ok(hipMemcpyAsync(S.d_in + i * slice, from, U.len, hipMemcpyHostToDevice, s_in), "H2D");
+      }
       rc = rc ? rc : hip_ok(hipEventRecord(S.ev_in, s_in), "event record");
       rc = rc ? rc : hip_ok(hipStreamWaitEvent(s_comp, S.ev_in, 0), "stream wait");
       ins.resize(nin);
@@ -255,8 +269,10 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
       if (rc == 0) rc = redset_hip::run_stripe(m, ins.data(), outs.data(), U.len, s_comp, 0);
       rc = rc ? rc : hip_ok(hipEventRecord(S.ev_comp, s_comp), "event record");
       rc = rc ? rc : hip_ok(hipStreamWaitEvent(s_out, S.ev_comp, 0), "stream wait");
-      for (size_t j = 0; j < nout && rc == 0; ++j)
-        rc = hip_ok(hipMemcpyAsync(S.h_out + j * slice, S.d_out + j * slice, U.len, hipMemcpyDeviceToHost, s_out), "D2H");
+      for (size_t j = 0; j < nout && rc == 0; ++j) {
+        void* to = S.dst[j] ? S.dst[j] : S.h_out + j * slice;
+        rc = hip_ok(hipMemcpyAsync(to, S.d_out + j * slice, U.len, hipMemcpyDeviceToHost, s_out), "D2H");
+      }
       rc = rc ? rc : hip_ok(hipEventRecord(S.ev_done, s_out), "event record");
       st.bytes_read += nin * U.len;
       st.bytes_written += nout * U.len;
@@ -321,6 +337,14 @@ struct redset_hip_hostio {
   std::vector<unsigned char*> lofi, parity;
   size_t stride;
 };
+
+namespace {
+void* hostio_map(void* ctx, int rank, int kind, int index, unsigned long long off) {
+  auto* h = static_cast<redset_hip_hostio*>(ctx);
+  unsigned char* base = kind == REDSET_HIP_CELL_DATA ? h->lofi[rank] : h->parity[rank];
+  return base + static_cast<size_t>(index) * h->stride + off;
+}
+}  // namespace
 
 namespace {
 int hostio_read(void* ctx, int rank, int kind, int index, unsigned long long off, size_t len, void* dst) {
@@ -478,7 +502,7 @@ int redset_hip_xor_rebuild_stream(int ranks, int root, size_t chunk_size, int fi
 }
 
 int redset_hip_hostio_create(int ranks, unsigned char* const* lofi, unsigned char* const* parity, size_t cell_stride,
-                             redset_hip_io* io_out, redset_hip_hostio** out) {
+                             int pinned, redset_hip_io* io_out, redset_hip_hostio** out) {
   if (!out || !io_out || !lofi || !parity || ranks < 1) return fail("hostio_create: bad argument");
   auto* h = new (std::nothrow) redset_hip_hostio;
   if (!h) return fail("out of host memory");
@@ -487,6 +511,7 @@ int redset_hip_hostio_create(int ranks, unsigned char* const* lofi, unsigned cha
   h->stride = cell_stride;
   io_out->read = hostio_read;
   io_out->write = hostio_write;
+  io_out->map = pinned ? hostio_map : nullptr;
   io_out->ctx = h;
   *out = h;
   return REDSET_SUCCESS;
@@ -530,6 +555,7 @@ int redset_hip_fileio_create(int ranks, const int* nfiles, const char* const* pa
   }
   io_out->read = fileio_read;
   io_out->write = fileio_write;
+  io_out->map = nullptr;
   io_out->ctx = f;
   *out = f;
   return REDSET_SUCCESS;

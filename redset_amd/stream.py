@@ -14,11 +14,11 @@ class HostIO:
     """Cells in host memory, laid out like the device set layout."""
 
     def __init__(self, ranks: int, lofi_ptrs: Sequence[int], parity_ptrs: Sequence[int], cell_stride: int,
-                 keepalive=()):
+                 keepalive=(), pinned: bool = False):
         self.io = _lib.StreamIO()
         h = c_void_p()
         _lib.check(_lib.load().redset_hip_hostio_create(
-            ranks, _lib.ptr_array(lofi_ptrs), _lib.ptr_array(parity_ptrs), cell_stride,
+            ranks, _lib.ptr_array(lofi_ptrs), _lib.ptr_array(parity_ptrs), cell_stride, int(pinned),
             ctypes.byref(self.io), ctypes.byref(h)), "hostio_create")
         self._h = h
         self._keep = keepalive

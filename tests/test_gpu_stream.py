@@ -168,3 +168,29 @@ def test_file_round_trip_crc(rd, oracle, tmp_path, scheme):
             assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
         got = np.fromfile(reds[r], dtype=np.uint8)[header[r]:header[r] + e * chunk]
         assert np.array_equal(got, want[r]), r
+
+
+@pytest.mark.parametrize("p,e,chunk", [(11, 3, 200_001), (20, 4, 65536)])
+def test_stream_direct_dma_pinned(rd, oracle, p, e, chunk):
+    """page-locked host cells are DMAed directly (no staging copy)"""
+    redset_amd, stream = rd
+    d = p - e
+    lofi_np, parity_np = oracle.random_set(p, d, e, chunk, seed=p * 3)
+    per = (d + e) * chunk
+    buf = torch.empty(p * per, dtype=torch.uint8, pin_memory=True)
+    for r in range(p):
+        buf[r * per:r * per + d * chunk].copy_(torch.from_numpy(lofi_np[r]))
+    base = buf.data_ptr()
+    io = stream.HostIO(p, [base + r * per for r in range(p)], [base + r * per + d * chunk for r in range(p)],
+                       chunk, keepalive=(buf,), pinned=True)
+    codec = redset_amd.RSCodec(p, e)
+    stream.rs_encode_stream(codec, chunk, io, slice_bytes=1 << 16)
+    oracle.OracleRS(p, e).encode_set(lofi_np, parity_np, chunk)
+    host = buf.numpy()
+    for r in range(p):
+        assert np.array_equal(host[r * per + d * chunk:(r + 1) * per], parity_np[r]), r
+    ref = buf.clone()
+    for r in (0, 7):
+        buf[r * per:(r + 1) * per].zero_()
+    stream.rs_rebuild_stream(codec, [0, 7], chunk, io, slice_bytes=1 << 16)
+    assert torch.equal(buf, ref)

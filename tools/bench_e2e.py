@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 MIB = 1 << 20
 
 
-def host_case(p, e, chunk, lost, slice_bytes, threads):
+def host_case(p, e, chunk, lost, slice_bytes, threads, pinned=True):
     import torch
     import redset_amd
     from redset_amd import stream
@@ -39,12 +39,12 @@ def host_case(p, e, chunk, lost, slice_bytes, threads):
     base = buf.data_ptr()
     lofi = [base + r * per for r in range(p)]
     parity = [base + r * per + d * chunk for r in range(p)]
-    io = stream.HostIO(p, lofi, parity, chunk, keepalive=(buf,))
+    io = stream.HostIO(p, lofi, parity, chunk, keepalive=(buf,), pinned=pinned)
     codec = redset_amd.RSCodec(p, e)
     out = []
     enc = stream.rs_encode_stream(codec, chunk, io, slice_bytes=slice_bytes, io_threads=threads)
     alg = p * (d + e) * chunk
-    out.append({"case": "host encode", "ranks": p, "encoding": e, "chunk": chunk, "GBps": alg / enc["seconds"] / 1e9,
+    out.append({"case": "host encode" + (" (direct DMA)" if pinned else " (staged)"), "ranks": p, "encoding": e, "chunk": chunk, "GBps": alg / enc["seconds"] / 1e9,
                 "stats": enc, "setup_s": setup})
     ref = buf[:per * p].clone() if p * per <= (64 << 30) else None
     for r in lost:
@@ -52,7 +52,7 @@ def host_case(p, e, chunk, lost, slice_bytes, threads):
     reb = stream.rs_rebuild_stream(codec, lost, chunk, io, slice_bytes=slice_bytes, io_threads=threads)
     alg_r = p * (d + len(lost)) * chunk
     ok = bool(torch.equal(buf, ref)) if ref is not None else None
-    out.append({"case": "host rebuild", "ranks": p, "encoding": e, "chunk": chunk, "lost": lost,
+    out.append({"case": "host rebuild" + (" (direct DMA)" if pinned else " (staged)"), "ranks": p, "encoding": e, "chunk": chunk, "lost": lost,
                 "GBps": alg_r / reb["seconds"] / 1e9, "stats": reb, "round_trip_equal": ok})
     return out
 
@@ -122,7 +122,8 @@ def main():
     lost = [int(x) for x in a.lost.split(",")]
     res = []
     if a.mode in ("host", "both"):
-        res += host_case(a.ranks, a.encoding, a.chunk_mib * MIB, lost, a.slice_mib * MIB, a.threads)
+        res += host_case(a.ranks, a.encoding, a.chunk_mib * MIB, lost, a.slice_mib * MIB, a.threads, pinned=True)
+        res += host_case(a.ranks, a.encoding, a.chunk_mib * MIB, lost, a.slice_mib * MIB, a.threads, pinned=False)
     if a.mode in ("disk", "both"):
         res += disk_case(a.ranks, a.encoding, a.disk_chunk_mib * MIB, lost, a.slice_mib * MIB, a.threads, a.dir)
     for r in res:

@@ -167,6 +167,8 @@ def main():
         step()
     torch.cuda.synchronize()
     if dist_on:
+        runner.reset_timing()
+    if dist_on:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()

@@ -76,6 +76,9 @@ class ShardedSetRunner:
         # bytes of my column slice of each cell (the last slice may be short)
         self.my_len = max(0, min(chunk, (rank + 1) * self.W) - rank * self.W)
         self.backend = backend if backend is not None else HipBackend(p, e)
+        self._place()
+        self.timing = self.device.type == "cuda"
+        self._events = []
         d, W, ph = self.d, self.W, p  # every GPU hosts p members
         u8 = dict(dtype=torch.uint8, device=self.device)
         self.D_host = torch.zeros(world, ph, d, W, **u8)
@@ -96,10 +99,23 @@ class ShardedSetRunner:
                     self._rebuild.append(self.backend.prepare_rebuild(views, self.lost, self.my_len, W))
 
     # ---- placement -------------------------------------------------------
+    def _place(self) -> None:
+        """member m of the world (set m // p, index m % p) lives on GPU
+        m % world; each GPU lists its hosted members with the lost ones last,
+        so an exchange can skip them with contiguous views."""
+        self._where = {}
+        self.n_alive = []
+        for g in range(self.world):
+            mine = [m for m in range(self.world * self.p) if m % self.world == g]
+            alive = [m for m in mine if (m % self.p) not in self.lost]
+            dead = [m for m in mine if (m % self.p) in self.lost]
+            for j, m in enumerate(alive + dead):
+                self._where[m] = (g, j)
+            self.n_alive.append(len(alive))
+
     def host_of(self, k: int, r: int):
         """(GPU, hosted index) of member r of set k."""
-        m = k * self.p + r
-        return m % self.world, m // self.world
+        return self._where[k * self.p + r]
 
     def set_views(self, k: int) -> SetViews:
         lofi, parity = [], []
@@ -110,11 +126,32 @@ class ShardedSetRunner:
         return SetViews(lofi, parity)
 
     # ---- exchanges -------------------------------------------------------
-    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor, skip_lost: bool = False) -> None:
+        """out[h] <- inp[me] of rank h, for every h. With skip_lost, the lost
+        members (hosted last, see host_of) are not sent: their cells are gone."""
         if self.world == 1:
             out.copy_(inp)
-        else:
+            return
+        if not skip_lost or not self.lost:
             dist.all_to_all_single(out, inp)
+            return
+        # uneven all-to-all as one batch of P2P ops (gloo has no uneven
+        # all_to_all; RCCL groups the batch into one launch)
+        me, n_send = self.rank, self.n_alive[self.rank]
+        out[me, :n_send].copy_(inp[me, :n_send])
+        ops = []
+        for g in range(self.world):
+            if g != me:
+                ops.append(dist.P2POp(dist.isend, inp[g, :n_send], g))
+                ops.append(dist.P2POp(dist.irecv, out[g, :self.n_alive[g]], g))
+        for req in dist.batch_isend_irecv(ops):
+            req.wait()
+
+    def _mark(self, name: str) -> None:
+        if self.timing:
+            ev = torch.cuda.Event(enable_timing=True)
+            ev.record()
+            self._events.append((name, ev))
 
     def _return_lost(self) -> None:
         """Send rebuilt slices of lost members to their hosts (the reference's
@@ -142,10 +179,14 @@ class ShardedSetRunner:
     def encode(self) -> None:
         """Parity of every stripe of every set: gather data slices, compute my
         column slice, return parity slices to their hosts."""
+        self._mark("encode_start")
         self._all_to_all(self.D_gath, self.D_host)
+        self._mark("encode_gathered")
         for fn in self._encode:
             fn()
+        self._mark("encode_computed")
         self._all_to_all(self.P_host, self.P_gath)
+        self._mark("encode_done")
 
     def erase(self) -> None:
         """Model the loss of the lost members' files on their hosts."""
@@ -158,11 +199,15 @@ class ShardedSetRunner:
 
     def rebuild(self) -> None:
         """Rebuild the lost members of every set from the survivors."""
-        self._all_to_all(self.D_gath, self.D_host)
-        self._all_to_all(self.P_gath, self.P_host)
+        self._mark("rebuild_start")
+        self._all_to_all(self.D_gath, self.D_host, skip_lost=True)
+        self._all_to_all(self.P_gath, self.P_host, skip_lost=True)
+        self._mark("rebuild_gathered")
         for fn in self._rebuild:
             fn()
+        self._mark("rebuild_computed")
         self._return_lost()
+        self._mark("rebuild_done")
 
     def step(self) -> None:
         self.encode()
@@ -178,21 +223,38 @@ class ShardedSetRunner:
 
     @property
     def exchanged_bytes(self) -> int:
-        """Bytes this GPU sends per step over the fabric."""
+        """Bytes this GPU sends per step over the fabric (average GPU)."""
         if self.world == 1:
             return 0
         frac = (self.world - 1) / self.world
-        p, d, e, C = self.p, self.d, self.e, self.chunk
+        p, d, e, C, m = self.p, self.d, self.e, self.chunk, len(self.lost)
         enc = (p * d + p * e) * C * frac
-        reb = (p * d + p * e) * C * frac + len(self.lost) * (d + e) * C * frac
+        reb = ((p - m) * (d + e) + m * (d + e)) * C * frac
         return int(enc + reb)
+
+    def phase_ms(self) -> dict:
+        """Mean milliseconds per phase over the steps marked so far."""
+        torch.cuda.synchronize()
+        acc, n = {}, {}
+        ev = self._events
+        for (a, ea), (b, eb) in zip(ev, ev[1:]):
+            if a.split("_")[0] != b.split("_")[0]:
+                continue
+            key = f"{a}->{b.split('_', 1)[1]}"
+            acc[key] = acc.get(key, 0.0) + ea.elapsed_time(eb)
+            n[key] = n.get(key, 0) + 1
+        return {k: round(acc[k] / n[k], 3) for k in acc}
+
+    def reset_timing(self) -> None:
+        self._events = []
 
     def report(self, step_seconds: float) -> dict:
         return {
             "exchange": {
                 "bytes_sent_per_gpu_per_step": self.exchanged_bytes,
                 "column_slice_bytes": self.W,
-                "collective": "all_to_all_single (RCCL) + batched P2P",
+                "collective": "RCCL all_to_all (data / parity slices) + batched P2P (rebuilt slices)",
+                "phase_ms_rank0": self.phase_ms() if self.timing else None,
             },
             "per_gpu_GBps": round(self.algorithmic_bytes / step_seconds / 1e9, 2),
         }

@@ -69,10 +69,18 @@ def _worker(rank, world, port, p, e, chunk, lost, outdir):
 
     runner = ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, device="cpu",
                               backend=OracleBackend(p, e), seed=99)
+    if rank == 0:
+        import json
+
+        with open(os.path.join(outdir, "where.json"), "w") as f:
+            json.dump({str(m): list(v) for m, v in runner._where.items()}, f)
     np.save(os.path.join(outdir, f"data_{rank}.npy"), runner.D_host.numpy())
     runner.encode()
     np.save(os.path.join(outdir, f"par_{rank}.npy"), runner.P_host.numpy())
     runner.erase()
+    # nothing from the encode may survive into the rebuild's gathered slices
+    runner.D_gath.fill_(0xA5)
+    runner.P_gath.fill_(0x5A)
     runner.rebuild()
     np.save(os.path.join(outdir, f"data2_{rank}.npy"), runner.D_host.numpy())
     np.save(os.path.join(outdir, f"par2_{rank}.npy"), runner.P_host.numpy())
@@ -80,10 +88,9 @@ def _worker(rank, world, port, p, e, chunk, lost, outdir):
     dist.destroy_process_group()
 
 
-def _assemble(host_arrays, world, p, chunk, W, k, r):
+def _assemble(host_arrays, where, world, p, chunk, W, k, r):
     """full cells of member r of set k from the per-GPU column slabs"""
-    m = k * p + r
-    h, j = m % world, m // world
+    h, j = where[str(k * p + r)]
     a = host_arrays[h]  # [g][j][cell][W]
     cells = []
     for c in range(a.shape[2]):
@@ -101,13 +108,17 @@ def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost):
         load = lambda name: [np.load(os.path.join(td, f"{name}_{g}.npy")) for g in range(world)]
         data, par, data2, par2 = load("data"), load("par"), load("data2"), load("par2")
         W = data[0].shape[-1]
+        import json
+
+        with open(os.path.join(td, "where.json")) as f:
+            where = json.load(f)
         st = oracle.OracleRS(p, e)
         for k in range(world):
-            lofi = [_assemble(data, world, p, chunk, W, k, r) for r in range(p)]
+            lofi = [_assemble(data, where, world, p, chunk, W, k, r) for r in range(p)]
             want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
             st.encode_set(lofi, want, chunk)
             for r in range(p):
-                assert np.array_equal(_assemble(par, world, p, chunk, W, k, r), want[r]), (k, r)
+                assert np.array_equal(_assemble(par, where, world, p, chunk, W, k, r), want[r]), (k, r)
                 # rebuild restored every member, lost ones included
-                assert np.array_equal(_assemble(data2, world, p, chunk, W, k, r), lofi[r]), (k, r)
-                assert np.array_equal(_assemble(par2, world, p, chunk, W, k, r), want[r]), (k, r)
+                assert np.array_equal(_assemble(data2, where, world, p, chunk, W, k, r), lofi[r]), (k, r)
+                assert np.array_equal(_assemble(par2, where, world, p, chunk, W, k, r), want[r]), (k, r)

@@ -203,7 +203,9 @@ void redset_hip_hostio_destroy(redset_hip_hostio* h);
  * dropped. Member r's parity goes to redundancy_paths[r] at
  * header_sizes[r] + slot*chunk_size (src/redset_reedsolomon.c:380-381).
  * Data files of members with writable[r] != 0 are created / extended to their
- * recorded size (rebuild targets); other data files are opened read-only. */
+ * recorded size (rebuild targets); other data files are opened read-only.
+ * redundancy_paths may be NULL (data-only I/O, e.g. for the per-rank MPI
+ * backends, which use their own fd_chunk). */
 typedef struct redset_hip_fileio redset_hip_fileio;
 int redset_hip_fileio_create(int ranks, const int* nfiles, const char* const* paths,
                              const unsigned long long* sizes, const char* const* redundancy_paths,

@@ -1,0 +1,56 @@
+/*
+ * redset_hip_mpi.h -- per-rank backends with the reference's calling
+ * convention, for MPI builds of redset (library libredset_hip_mpi.so).
+ *
+ * These are what the reference's backend slot calls per rank
+ * (src/redset_internal.h:345-381: redset_{reedsolomon,xor}_{encode,decode}_gpu),
+ * with redset's own types replaced by plain arguments:
+ *   d->comm / d->ranks / d->rank   -> comm (its size and rank)
+ *   d->state (GF tables, mat)      -> rs (redset_hip_rs_create(ranks, encoding))
+ *   redset_lofi rsf                -> lofi: this rank's logical file as a
+ *                                     redset_hip_io (rank argument 0; kind DATA,
+ *                                     index = segment, offset within segment)
+ *   chunk_file, fd_chunk           -> same; fd_chunk is positioned just after
+ *                                     the header on entry and the header size is
+ *                                     taken as lseek(fd_chunk, 0, SEEK_CUR)
+ *                                     (src/redset_reedsolomon.c:295, :588)
+ *   redset_mpi_buf_size            -> buf_size (0 = 1 MiB, src/redset.c:45)
+ * The message pattern of every MPI exchange is the reference's (RS encode
+ * ring :329-363, RS decode ring + gather :646-733); XOR uses one all-to-all
+ * per slice for encode and a gather to the root for decode (same bytes as
+ * the reference's pipelined rings). All arithmetic runs on the GPU.
+ * Collective over comm; returns REDSET_SUCCESS / REDSET_FAILURE; I/O errors
+ * fail the call but the collective loop continues, as in the reference.
+ */
+#ifndef REDSET_HIP_MPI_H
+#define REDSET_HIP_MPI_H
+
+#include <mpi.h>
+
+#include "redset_hip.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* replaces redset_reedsolomon_encode (src/redset_reedsolomon.c:280-402) */
+int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi,
+                              const char* chunk_file, int fd_chunk, size_t chunk_size, size_t buf_size);
+
+/* replaces redset_reedsolomon_decode (src/redset_reedsolomon.c:570-785) */
+int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missing, const int* rebuild_ranks,
+                              int need_rebuild, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
+                              size_t chunk_size, size_t buf_size);
+
+/* replaces redset_xor_encode (src/redset_xor.c:220-295) */
+int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
+                               size_t chunk_size, size_t buf_size);
+
+/* replaces redset_xor_decode (src/redset_xor.c:441-531) */
+int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
+                               int fd_chunk, size_t chunk_size, size_t buf_size);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* REDSET_HIP_MPI_H */

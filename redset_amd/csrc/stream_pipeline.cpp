@@ -441,6 +441,7 @@ int fileio_read(void* ctx, int rank, int kind, int index, unsigned long long off
   auto* f = static_cast<redset_hip_fileio*>(ctx);
   if (kind == REDSET_HIP_CELL_DATA)
     return lofi_rw(f, rank, static_cast<unsigned long long>(index) * f->chunk + off, len, static_cast<char*>(dst), false);
+  if (f->red_fd[rank] < 0) return -1;
   return full_pread(f->red_fd[rank], dst, len, static_cast<off_t>(f->header[rank] + index * f->chunk + off));
 }
 
@@ -449,6 +450,7 @@ int fileio_write(void* ctx, int rank, int kind, int index, unsigned long long of
   if (kind == REDSET_HIP_CELL_DATA)
     return lofi_rw(f, rank, static_cast<unsigned long long>(index) * f->chunk + off, len,
                    const_cast<char*>(static_cast<const char*>(src)), true);
+  if (f->red_fd[rank] < 0) return -1;
   return full_pwrite(f->red_fd[rank], src, len, static_cast<off_t>(f->header[rank] + index * f->chunk + off));
 }
 
@@ -523,8 +525,7 @@ int redset_hip_fileio_create(int ranks, const int* nfiles, const char* const* pa
                              const char* const* redundancy_paths, const unsigned long long* header_sizes,
                              size_t chunk_size, const int* writable, redset_hip_io* io_out,
                              redset_hip_fileio** out) {
-  if (!out || !io_out || !nfiles || !paths || !sizes || !redundancy_paths || ranks < 1)
-    return fail("fileio_create: bad argument");
+  if (!out || !io_out || !nfiles || !paths || !sizes || ranks < 1) return fail("fileio_create: bad argument");
   auto* f = new (std::nothrow) redset_hip_fileio;
   if (!f) return fail("out of host memory");
   f->chunk = chunk_size;
@@ -546,6 +547,7 @@ int redset_hip_fileio_create(int ranks, const int* nfiles, const char* const* pa
     }
     if (rc) break;
     f->header[r] = header_sizes ? header_sizes[r] : 0;
+    if (!redundancy_paths || !redundancy_paths[r]) continue;  // data-only I/O (per-rank backends)
     f->red_fd[r] = ::open(redundancy_paths[r], O_RDWR | O_CREAT, 0600);
     if (f->red_fd[r] < 0) rc = fail("open(%s): %s", redundancy_paths[r], strerror(errno));
   }

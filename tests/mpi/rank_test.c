@@ -1,0 +1,111 @@
+/*
+ * rank_test.c -- one MPI rank of a redundancy set, driving the per-rank
+ * backends of libredset_hip_mpi.so exactly as redset_apply_rs /
+ * redset_recover_rs_rebuild drive a backend (src/redset_reedsolomon.c:
+ * 498-545, :826-1006): open the redundancy file, write (or skip) a header,
+ * leave fd_chunk positioned after it, call the backend, fsync + close.
+ *
+ * usage: rank_test <rs|xor> <encode|rebuild> <encoding> <dir> <buf_bytes> [lost ranks...]
+ * Rank r reads <dir>/manifest_<r>.txt:
+ *   nfiles \n path size \n ... chunk_size \n header_size \n redundancy_path
+ * (written by tests/test_gpu_mpi.py). Exit 0 iff every rank succeeded.
+ */
+#include <fcntl.h>
+#include <mpi.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "redset_hip.h"
+#include "redset_hip_mpi.h"
+
+int main(int argc, char** argv) {
+  MPI_Init(&argc, &argv);
+  int rank, ranks;
+  MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+  MPI_Comm_size(MPI_COMM_WORLD, &ranks);
+  if (argc < 6) {
+    if (rank == 0) fprintf(stderr, "usage: %s rs|xor encode|rebuild encoding dir buf [lost...]\n", argv[0]);
+    MPI_Abort(MPI_COMM_WORLD, 2);
+  }
+  const int rs_scheme = strcmp(argv[1], "rs") == 0;
+  const int encode = strcmp(argv[2], "encode") == 0;
+  const int encoding = atoi(argv[3]);
+  const char* dir = argv[4];
+  const size_t buf = (size_t) atoll(argv[5]);
+  int missing = argc - 6;
+  int lost[256];
+  int need_rebuild = 0;
+  for (int i = 0; i < missing; ++i) {
+    lost[i] = atoi(argv[6 + i]);
+    if (lost[i] == rank) need_rebuild = 1;
+  }
+
+  char path[4096];
+  snprintf(path, sizeof(path), "%s/manifest_%d.txt", dir, rank);
+  FILE* mf = fopen(path, "r");
+  if (!mf) MPI_Abort(MPI_COMM_WORLD, 3);
+  int nfiles = 0;
+  if (fscanf(mf, "%d", &nfiles) != 1) MPI_Abort(MPI_COMM_WORLD, 3);
+  char** paths = calloc(nfiles + 1, sizeof(char*));
+  unsigned long long* sizes = calloc(nfiles + 1, sizeof(unsigned long long));
+  for (int i = 0; i < nfiles; ++i) {
+    paths[i] = malloc(4096);
+    if (fscanf(mf, "%4095s %llu", paths[i], &sizes[i]) != 2) MPI_Abort(MPI_COMM_WORLD, 3);
+  }
+  unsigned long long chunk = 0, header = 0;
+  char red[4096];
+  if (fscanf(mf, "%llu %llu %4095s", &chunk, &header, red) != 3) MPI_Abort(MPI_COMM_WORLD, 3);
+  fclose(mf);
+
+  /* this rank's logical file (redset_lofi_open, src/redset_lofi.c:306-405) */
+  redset_hip_io io;
+  redset_hip_fileio* files = NULL;
+  int writable = encode ? 0 : need_rebuild;
+  int rc = redset_hip_fileio_create(1, &nfiles, (const char* const*) paths, sizes, NULL, NULL, (size_t) chunk,
+                                    &writable, &io, &files);
+  if (rc != REDSET_SUCCESS) {
+    fprintf(stderr, "rank %d: fileio: %s\n", rank, redset_hip_last_error());
+    MPI_Abort(MPI_COMM_WORLD, 4);
+  }
+
+  /* redundancy file: header first, backend writes after it */
+  int fd;
+  if (encode || need_rebuild) {
+    fd = open(red, O_RDWR | O_CREAT | O_TRUNC, 0600);
+    char* h = malloc(header ? header : 1);
+    memset(h, 'H', header);
+    if (fd < 0 || write(fd, h, header) != (ssize_t) header) MPI_Abort(MPI_COMM_WORLD, 5);
+    free(h);
+  } else {
+    fd = open(red, O_RDONLY);
+    if (fd < 0 || lseek(fd, (off_t) header, SEEK_SET) < 0) MPI_Abort(MPI_COMM_WORLD, 5);
+  }
+
+  if (rs_scheme) {
+    redset_hip_rs* rs = NULL;
+    rc = redset_hip_rs_create(ranks, encoding, &rs);
+    if (rc == REDSET_SUCCESS) {
+      rc = encode ? redset_hip_rs_encode_rank(rs, MPI_COMM_WORLD, &io, red, fd, chunk, buf)
+                  : redset_hip_rs_decode_rank(rs, MPI_COMM_WORLD, missing, lost, need_rebuild, &io, red, fd,
+                                              chunk, buf);
+    }
+    redset_hip_rs_destroy(rs);
+  } else {
+    rc = encode ? redset_hip_xor_encode_rank(MPI_COMM_WORLD, &io, red, fd, chunk, buf)
+                : redset_hip_xor_decode_rank(MPI_COMM_WORLD, missing ? lost[0] : 0, &io, red, fd, chunk, buf);
+  }
+  if (rc != REDSET_SUCCESS) fprintf(stderr, "rank %d: backend failed: %s\n", rank, redset_hip_last_error());
+  fsync(fd);
+  close(fd);
+  redset_hip_fileio_destroy(files);
+
+  int ok = rc == REDSET_SUCCESS, all = 0;
+  MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_LAND, MPI_COMM_WORLD); /* redset_alltrue */
+  for (int i = 0; i < nfiles; ++i) free(paths[i]);
+  free(paths);
+  free(sizes);
+  MPI_Finalize();
+  return all ? 0 : 1;
+}

@@ -1,0 +1,111 @@
+"""GPU + MPI tests of the per-rank backends (libredset_hip_mpi.so): a set of
+P MPI processes (sharing the GPU) run redset's per-rank encode / rebuild
+calling convention through tests/mpi/rank_test.c. Checks: parity after the
+header equals the oracle's on the ranks' padded logical files, and a rebuild
+after deleting ranks' files restores them with identical CRC32
+(test/test_redset.c:459-589 semantics)."""
+import os
+import shutil
+import subprocess
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+RANK_TEST = os.path.join(ROOT, "tests", "mpi", "build", "rank_test")
+MPIRUN = "/opt/conda/bin/mpirun"
+
+
+def _have():
+    try:
+        import torch
+
+        if not torch.cuda.is_available():
+            return False
+    except Exception:
+        return False
+    if not os.path.exists(MPIRUN):
+        return False
+    if not os.path.exists(RANK_TEST):
+        subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "tests", "mpi")], check=False)
+    return os.path.exists(RANK_TEST)
+
+
+def _mpirun(np_, args, timeout=300):
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", RANK_TEST] + [str(a) for a in args]
+    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+
+
+def _setup(tmp, p, d, rng, maxsize):
+    files = []
+    for r in range(p):
+        fl = []
+        for k in range(int(rng.integers(1, 4))):
+            size = int(rng.integers(0, maxsize))
+            path = os.path.join(tmp, f"r{r}_f{k}.dat")
+            rng.integers(0, 256, size, dtype=np.uint8).tofile(path)
+            fl.append((path, size))
+        files.append(fl)
+    max_bytes = max(sum(s for _, s in f) for f in files)
+    chunk = max(1, -(-max_bytes // d))  # src/redset_reedsolomon.c:485-493
+    return files, chunk
+
+
+def _manifests(tmp, files, chunk, header, reds):
+    for r, fl in enumerate(files):
+        with open(os.path.join(tmp, f"manifest_{r}.txt"), "w") as f:
+            f.write(f"{len(fl)}\n")
+            for path, size in fl:
+                f.write(f"{path} {size}\n")
+            f.write(f"{chunk}\n{header[r]}\n{reds[r]}\n")
+
+
+def _logical(fl, total):
+    cat = np.concatenate([np.fromfile(p, dtype=np.uint8) for p, _ in fl]) if fl else np.zeros(0, np.uint8)
+    out = np.zeros(total, np.uint8)
+    out[:cat.size] = cat
+    return out
+
+
+@pytest.mark.parametrize("scheme,p,e,lost,buf", [("rs", 6, 2, [1, 4], 65536), ("rs", 5, 3, [0, 2, 4], 40000),
+                                                  ("xor", 4, 1, [2], 50000)])
+def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf):
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    tmp = str(tmp_path)
+    d = p - e
+    rng = np.random.default_rng(p * 10 + e)
+    files, chunk = _setup(tmp, p, d, rng, 200_000)
+    header = [1000 + 7 * r for r in range(p)]
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, header, reds)
+    crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
+
+    res = _mpirun(p, [scheme, "encode", e, tmp, buf])
+    assert res.returncode == 0, res.stdout + res.stderr
+    lofi = [_logical(fl, d * chunk) for fl in files]
+    want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+    if scheme == "rs":
+        oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    else:
+        oracle.xor_encode_set(p, lofi, want, chunk)
+    for r in range(p):
+        blob = np.fromfile(reds[r], dtype=np.uint8)
+        assert blob.size == header[r] + e * chunk
+        assert np.array_equal(blob[header[r]:], want[r]), r
+
+    # lose ranks: files and redundancy file gone (fault injection by unlink)
+    for r in lost:
+        for path, _ in files[r]:
+            os.unlink(path)
+        os.unlink(reds[r])
+    res = _mpirun(p, [scheme, "rebuild", e, tmp, buf] + lost)
+    assert res.returncode == 0, res.stdout + res.stderr
+    for r in lost:
+        for path, size in files[r]:
+            assert os.path.getsize(path) == size
+            assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
+        blob = np.fromfile(reds[r], dtype=np.uint8)
+        assert np.array_equal(blob[header[r]:header[r] + e * chunk], want[r]), r

@@ -351,11 +351,13 @@ def test_sharded_runner_world1_hip(rd, oracle):
     run.encode()
     torch.cuda.synchronize()
     par = run.P_host.cpu().numpy()
-    lofi = [np.ascontiguousarray(data[0, r, :, :chunk]).reshape(-1) for r in range(p)]
+    # hosted index of member r (lost members are hosted last)
+    j = [run.host_of(0, r)[1] for r in range(p)]
+    lofi = [np.ascontiguousarray(data[0, j[r], :, :chunk]).reshape(-1) for r in range(p)]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
     for r in range(p):
-        assert np.array_equal(np.ascontiguousarray(par[0, r, :, :chunk]).reshape(-1), want[r])
+        assert np.array_equal(np.ascontiguousarray(par[0, j[r], :, :chunk]).reshape(-1), want[r])
     run.erase()
     run.rebuild()
     torch.cuda.synchronize()

@@ -398,6 +398,97 @@ float run_pipe(const Setup& S, int blocks_per_cu, int cus, int reps, double byte
   return ms;
 }
 
+
+// PIPE with buffer loads/stores carrying explicit cache-policy bits
+// (aux: 1 = sc0, 2 = nt, 16 = sc1)
+template <int NIN, int LAUX, int SAUX>
+__global__ void __launch_bounds__(256) kpipe_aux(const Job* jobs, size_t nvec, int bpj, int nout) {
+  __shared__ uint32_t lds[NIN * 32];
+  const int job = blockIdx.x / bpj;
+  const int part = blockIdx.x - job * bpj;
+  const Job& J = jobs[job];
+  for (int e = threadIdx.x; e < NIN * 32; e += 256) {
+    const int i = e >> 5, h = (e >> 4) & 1;
+    const uint32_t x = static_cast<uint32_t>(e & 15) << (4 * h);
+    uint32_t v = 0;
+    for (int j = 0; j < nout; ++j) v |= gf_mul_dev(J.coef[j][i], x) << (8 * j);
+    lds[e] = v;
+  }
+  __syncthreads();
+  const int nrec = (int)(nvec * 16 > 0x7fffffffull ? 0x7fffffff : nvec * 16);
+  __amdgpu_buffer_rsrc_t rin[NIN], rout[kMaxOut];
+#pragma unroll
+  for (int i = 0; i < NIN; ++i) rin[i] = __builtin_amdgcn_make_buffer_rsrc((void*)J.in[i], 0, nrec, 0x00020000);
+#pragma unroll
+  for (int j = 0; j < kMaxOut; ++j) rout[j] = __builtin_amdgcn_make_buffer_rsrc((void*)J.out[j], 0, nrec, 0x00020000);
+  const size_t vstep = (size_t)bpj * 256;
+  size_t v = (size_t)part * 256 + threadIdx.x;
+  v4u x[NIN];
+  if (v < nvec) {
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) x[i] = __builtin_amdgcn_raw_buffer_load_b128(rin[i], (int)(v * 16), 0, LAUX);
+  }
+  for (; v < nvec; v += vstep) {
+    const size_t vn = v + vstep;
+    v4u xn[NIN];
+    if (vn < nvec) {
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) xn[i] = __builtin_amdgcn_raw_buffer_load_b128(rin[i], (int)(vn * 16), 0, LAUX);
+    }
+    uint32_t acc[16];
+#pragma unroll
+    for (int b = 0; b < 16; ++b) acc[b] = 0;
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) {
+      const uint32_t w[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t lo4 = (w[q] << 2) & 0x3C3C3C3Cu;
+        const uint32_t hi4 = (w[q] >> 2) & 0x3C3C3C3Cu;
+        const uint32_t ol[4] = {byte_of<0>(lo4), byte_of<8>(lo4), byte_of<16>(lo4), byte_of<24>(lo4)};
+        const uint32_t oh[4] = {byte_of<0>(hi4), byte_of<8>(hi4), byte_of<16>(hi4), byte_of<24>(hi4)};
+#pragma unroll
+        for (int b = 0; b < 4; ++b)
+          acc[4 * q + b] = xor3(acc[4 * q + b], lds_at(lds, i * 128 + ol[b]), lds_at(lds, i * 128 + 64 + oh[b]));
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < kMaxOut; ++j) {
+      if (j < nout) {
+        v4u r;
+        r.x = gather_byte(acc[0], acc[1], acc[2], acc[3], j);
+        r.y = gather_byte(acc[4], acc[5], acc[6], acc[7], j);
+        r.z = gather_byte(acc[8], acc[9], acc[10], acc[11], j);
+        r.w = gather_byte(acc[12], acc[13], acc[14], acc[15], j);
+        __builtin_amdgcn_raw_buffer_store_b128(r, rout[j], (int)(v * 16), 0, SAUX);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) x[i] = xn[i];
+  }
+}
+
+template <int LAUX, int SAUX>
+float run_aux(const Setup& S, int blocks_per_cu, int cus, int reps, double bytes) {
+  const int njobs = (int)S.jobs.size();
+  int bpj = (cus * blocks_per_cu) / njobs;
+  hipEvent_t a, b;
+  CHECK(hipEventCreate(&a));
+  CHECK(hipEventCreate(&b));
+  for (int i = 0; i < 3; ++i) hipLaunchKernelGGL((kpipe_aux<8, LAUX, SAUX>), dim3(njobs * bpj), dim3(256), 0, 0, S.d_jobs, S.nvec, bpj, S.nout);
+  CHECK(hipDeviceSynchronize());
+  CHECK(hipEventRecord(a));
+  for (int i = 0; i < reps; ++i) hipLaunchKernelGGL((kpipe_aux<8, LAUX, SAUX>), dim3(njobs * bpj), dim3(256), 0, 0, S.d_jobs, S.nvec, bpj, S.nout);
+  CHECK(hipEventRecord(b));
+  CHECK(hipEventSynchronize(b));
+  float ms = 0;
+  CHECK(hipEventElapsedTime(&ms, a, b));
+  ms /= reps;
+  printf("%-30s laux=%2d saux=%2d bpc=%d  %8.4f ms  %8.1f GB/s\n", "PIPE buffer-op", LAUX, SAUX, blocks_per_cu, ms, bytes / (ms * 1e-3) / 1e9);
+  fflush(stdout);
+  return ms;
+}
+
 int main(int argc, char** argv) {
   const size_t C = (argc > 1 ? atol(argv[1]) : 64) << 20;
   const size_t pad = argc > 2 ? atol(argv[2]) : 0;        // bytes between consecutive cells
@@ -465,9 +556,17 @@ int main(int argc, char** argv) {
       printf("%-44s grid=%d  %8.4f ms  %8.1f GB/s\n", "copy (1 in -> 1 out, float4)", g, ms, (double)total / (ms * 1e-3) / 1e9);
     }
   }
-  {
+  for (int round = 0; round < (getenv("GFBENCH_ROUNDS") ? atoi(getenv("GFBENCH_ROUNDS")) : 1); ++round) {
+    printf("round %d\n", round);
     run<8, MEMONLY, false, 1, 256, true>(S, 2, cus, reps, "memonly GS", bytes);
     run_pipe(S, 4, cus, reps, bytes);
+    run_aux<0, 0>(S, 4, cus, reps, bytes);
+    run_aux<2, 0>(S, 4, cus, reps, bytes);
+    run_aux<0, 2>(S, 4, cus, reps, bytes);
+    run_aux<0, 19>(S, 4, cus, reps, bytes);
+    run_aux<2, 19>(S, 4, cus, reps, bytes);
+    run_aux<0, 17>(S, 4, cus, reps, bytes);
+    run_aux<16, 0>(S, 4, cus, reps, bytes);
   }
   }  // allocations (kept live so each one gets new physical pages)
   return 0;

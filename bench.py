@@ -9,11 +9,15 @@ members {1, 2} from the survivors. Both passes run the gf_mac HIP kernel.
 (10^9 B). Algorithmic bytes per stripe: encode (d + e)*C, rebuild (d + m)*C
 (SURVEY.md §8d).
 
-N>1 (torchrun, one process per GPU, RCCL): weak scaling -- every GPU hosts 11
-members; the world holds N sets whose members are spread round-robin over the
-GPUs, and every stripe is computed column-sharded over all GPUs after an
-all-to-all gather of cell slices (redset_amd.dist); the exchange is inside the
-timed step.
+N>1 (torchrun, one process per GPU, RCCL): weak scaling. Redundancy sets are
+independent objects, so the timed step shards them across ranks with no
+data-path collective: every GPU encodes + rebuilds its own set exactly as at
+N=1, and `value` = all ranks' algorithmic bytes / the max-over-ranks step
+time. The path's one real exchange -- the multi-rank rebuild whose chunks are
+gathered over xGMI -- is measured after it as a second timed
+leg and reported under "sharded": N sets whose members are spread round-robin
+over the GPUs, every stripe computed column-sharded over all GPUs after an
+RCCL all-to-all of cell slices (redset_amd.dist), exchange inside the timing.
 
 Prints ONE JSON line on rank 0.
 """
@@ -104,6 +108,36 @@ def load_traffic(path, kernel_prefix):
         return None
 
 
+def timed(step, steps, warmup, dist_on, before=None):
+    """W untimed warmups, then K steps bracketed by barrier + synchronize on
+    both sides; returns the max-over-ranks elapsed seconds."""
+    import torch
+
+    for _ in range(warmup):
+        step(-1)
+    torch.cuda.synchronize()
+    if before is not None:
+        before()
+    if dist_on:
+        import torch.distributed as dist
+
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        step(k)
+    torch.cuda.synchronize()
+    if dist_on:
+        dist.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if dist_on:
+        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed
+
+
 def main():
     args = parse()
     import torch
@@ -131,62 +165,34 @@ def main():
     lost = sorted(int(x) for x in args.lost.split(",") if x != "")
     stream = torch.cuda.current_stream()
 
-    if dist_on:
-        from redset_amd import dist as rdist
+    # this rank's own set, all cells resident in HBM
+    codec = redset_amd.RSCodec(p, e)
+    lay = redset_amd.SetLayout.allocate(p, d, e, chunk)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(1234 + rank)
+    for r in range(p):
+        n = lay.lofi(r).numel()
+        lay.lofi(r).copy_(torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g))
+    enc_plan = codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    reb_plan = codec.plan_rebuild(lost, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    eb = enc_plan.bytes_read + enc_plan.bytes_written
+    rb = reb_plan.bytes_read + reb_plan.bytes_written
+    bytes_per_step = eb + rb
+    ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
 
-        runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank)
-        step = runner.step
-        bytes_per_step = runner.algorithmic_bytes * world
-    else:
-        codec = redset_amd.RSCodec(p, e)
-        lay = redset_amd.SetLayout.allocate(p, d, e, chunk)
-        g = torch.Generator(device="cuda")
-        g.manual_seed(1234)
-        for r in range(p):
-            n = lay.lofi(r).numel()
-            lay.lofi(r).copy_(torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g))
-        enc_plan = codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
-        reb_plan = codec.plan_rebuild(lost, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
-        bytes_per_step = (enc_plan.bytes_read + enc_plan.bytes_written
-                          + reb_plan.bytes_read + reb_plan.bytes_written)
-        ev = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(args.steps)]
-        cur = {"i": -1}
+    def step(i):
+        if i >= 0:
+            ev[i][0].record(stream)
+        enc_plan.execute(stream)
+        if i >= 0:
+            ev[i][1].record(stream)
+        reb_plan.execute(stream)
+        if i >= 0:
+            ev[i][2].record(stream)
 
-        def step():
-            i = cur["i"]
-            if i >= 0:
-                ev[i][0].record(stream)
-            enc_plan.execute(stream)
-            if i >= 0:
-                ev[i][1].record(stream)
-            reb_plan.execute(stream)
-            if i >= 0:
-                ev[i][2].record(stream)
-
-    for _ in range(args.warmup):
-        step()
-    torch.cuda.synchronize()
-    if dist_on:
-        runner.reset_timing()
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        if not dist_on:
-            cur["i"] = k
-        step()
-    torch.cuda.synchronize()
-    if dist_on:
-        dist.barrier()
-    torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    if dist_on:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = timed(step, args.steps, args.warmup, dist_on)
     ms_per_step = elapsed * 1e3 / args.steps
-    value = bytes_per_step / (elapsed / args.steps) / 1e9
+    value = world * bytes_per_step / (elapsed / args.steps) / 1e9
 
     result = {
         "metric": "GB/s device-resident RS/XOR encode+rebuild vs HBM peak, 1/2/4/8 MI355X",
@@ -203,46 +209,57 @@ def main():
         "data": "synthetic: uniform random bytes (torch.randint on device), all cells resident in HBM",
         "config": {
             "workload": (f"RS({d}+{e}) p={p} e={e}, chunk {args.chunk_mib:g} MiB: full-set encode of all "
-                         f"{p} stripes + rebuild of members {lost}"),
+                         f"{p} stripes + rebuild of members {lost}, one set per GPU"),
             "ranks": p,
             "encoding": e,
             "chunk_bytes": chunk,
             "sets": world,
-            "bytes_per_step": bytes_per_step,
-            "parallelism": "single GPU" if world == 1 else f"column-sharded over {world} GPUs, RCCL all-to-all",
+            "bytes_per_step_per_gpu": bytes_per_step,
+            "parallelism": "single GPU" if world == 1 else f"{world} independent sets, one per GPU (no collective)",
         },
     }
-    if not dist_on:
-        enc_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
-        reb_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
-        eb = enc_plan.bytes_read + enc_plan.bytes_written
-        rb = reb_plan.bytes_read + reb_plan.bytes_written
-        achieved = (eb + rb) / ((enc_ms + reb_ms) * 1e-3) / 1e9
-        # PMC-measured HBM bytes per gf_mac launch, averaged over the step's
-        # encode and rebuild launches (tools/pmc_traffic.py; gfx950 FETCH_SIZE
-        # doubled); compare with the algorithmic average below
-        traffic = load_traffic(args.traffic_json, "gf_mac_kernel<8>")
-        result["roofline"] = {
-            "bound": "hbm",
-            "kernel": "gf_mac_kernel<8> (redset_amd/csrc/codec_kernels.hip)",
-            "achieved": round(achieved, 1),
-            "peak": HBM_PEAK_GBPS,
+    enc_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
+    reb_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
+    achieved = (eb + rb) / ((enc_ms + reb_ms) * 1e-3) / 1e9
+    # PMC-measured HBM bytes per gf_mac launch, averaged over the step's
+    # encode and rebuild launches (tools/pmc_traffic.py; gfx950 FETCH_SIZE
+    # doubled); compare with the algorithmic average below
+    traffic = load_traffic(args.traffic_json, "gf_mac_kernel<8>")
+    result["roofline"] = {
+        "bound": "hbm",
+        "kernel": "gf_mac_kernel<8> (redset_amd/csrc/codec_kernels.hip)",
+        "achieved": round(achieved, 1),
+        "peak": HBM_PEAK_GBPS,
+        "unit": "GB/s",
+        "frac": round(achieved / HBM_PEAK_GBPS, 4),
+        "traffic": traffic,
+        "algorithmic_bytes_per_launch": {"encode": eb, "rebuild": rb, "mean": (eb + rb) // 2},
+        "traffic_source": "profiles/traffic_latest.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
+        "avg_launch_ms": {"encode": round(enc_ms, 4), "rebuild": round(reb_ms, 4)},
+    }
+    result["breakdown"] = {
+        "encode_GBps": round(eb / (enc_ms * 1e-3) / 1e9, 1),
+        "encode_read_GBps": round(enc_plan.bytes_read / (enc_ms * 1e-3) / 1e9, 1),
+        "rebuild_GBps": round(rb / (reb_ms * 1e-3) / 1e9, 1),
+    }
+    if dist_on:
+        # second leg: the multi-rank rebuild with its RCCL exchange
+        from redset_amd import dist as rdist
+
+        runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank)
+        s_elapsed = timed(lambda i: runner.step(), args.steps, args.warmup, dist_on, before=runner.reset_timing)
+        s_step = s_elapsed / args.steps
+        sharded = {
+            "workload": (f"{world} sets of p={p}, members round-robin over {world} GPUs; encode + rebuild of "
+                         f"members {lost} of every set, column-sharded, RCCL all-to-all + batched P2P"),
+            "value": round(world * runner.algorithmic_bytes / s_step / 1e9, 2),
             "unit": "GB/s",
-            "frac": round(achieved / HBM_PEAK_GBPS, 4),
-            "traffic": traffic,
-            "algorithmic_bytes_per_launch": {"encode": eb, "rebuild": rb, "mean": (eb + rb) // 2},
-            "traffic_source": "profiles/traffic_latest.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
-            "avg_launch_ms": {"encode": round(enc_ms, 4), "rebuild": round(reb_ms, 4)},
+            "ms_per_step": round(s_step * 1e3, 4),
         }
-        result["breakdown"] = {
-            "encode_GBps": round(eb / (enc_ms * 1e-3) / 1e9, 1),
-            "encode_read_GBps": round(enc_plan.bytes_read / (enc_ms * 1e-3) / 1e9, 1),
-            "rebuild_GBps": round(rb / (reb_ms * 1e-3) / 1e9, 1),
-        }
-        if args.cpu_baseline and rank == 0:
-            result["cpu_baseline"] = cpu_baseline(p, e, lost, args.cpu_seconds)
-    else:
-        result.update(runner.report(elapsed / args.steps))
+        sharded.update(runner.report(s_step))
+        result["sharded"] = sharded
+    if args.cpu_baseline and rank == 0 and not dist_on:
+        result["cpu_baseline"] = cpu_baseline(p, e, lost, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist_on:

@@ -11,7 +11,9 @@ import ctypes
 import os
 from ctypes import POINTER, c_char_p, c_int, c_size_t, c_ubyte, c_ulonglong, c_void_p
 
-LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "lib", "libredset_hip.so")
+# REDSET_HIP_LIBRARY points at another build of the same library (A/B runs)
+LIB_PATH = os.environ.get("REDSET_HIP_LIBRARY") or os.path.join(
+    os.path.dirname(os.path.abspath(__file__)), "lib", "libredset_hip.so")
 
 REDSET_SUCCESS = 0
 REDSET_FAILURE = 1

@@ -1,0 +1,320 @@
+// codec_device.h -- CDNA4 (gfx950) kernels for redset's RS / XOR codec.
+//
+// gf_mac: out[j] = sum_i coef[j][i] * in[i] over GF(2^8)/0x11D, byte-wise.
+//   Replaces the reference's e*d separate read-modify-write passes of
+//   redset_rs_reduce_buffer_multadd (src/redset_reedsolomon_common.c:786-819;
+//   CUDA multadd_gpu, src/redset_reedsolomon_gpu.cu:29-48) with ONE pass that
+//   reads every input once and writes every output once.
+//
+//   Multiplication by a constant is GF(2)-linear, so c*x = c*(x & 0x0F) ^
+//   c*(x & 0xF0). For every input i the block builds two 16-entry nibble
+//   tables in LDS whose entries pack the products for all (<= 4) outputs into
+//   one dword: T_i,h[n] = sum_j (coef[j][i] * (n << 4h)) << 8j. A byte then
+//   costs two ds_read_b32 and two XORs for all outputs at once. A 16-entry
+//   dword table spans 16 distinct banks, so whatever the data a wave's reads
+//   of it are conflict-free (equal nibbles broadcast); no replication needed.
+//   Inputs stream in as 16-B loads (1 KiB per wave instruction); the 16
+//   packed accumulators are transposed back to per-output bytes with v_perm.
+//
+// xor_reduce: out = XOR of inputs (reference reduce_xor, src/redset_xor.c:35-42;
+//   CUDA xor_gpu, src/redset_xor_gpu.cu:20-26), one pass, 16-B vectors.
+//
+// Kernel templates only; every codec_sets_*.hip instantiates them for a
+// range of input counts (split so the instantiations compile in parallel)
+// and exposes them through a KernelSet table (codec_kernels.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include "codec_kernels.h"
+
+namespace redset_hip {
+
+namespace {
+
+
+__device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    r ^= (b & 1u) ? a : 0u;
+    b >>= 1;
+    a <<= 1;
+    a ^= (a & 0x100u) ? 0x11Du : 0u;
+  }
+  return r;
+}
+
+// LDS image: [input][half][nibble] dwords = 128 B per input.
+constexpr int kTableBytes = 2 * 16 * 4;
+
+__device__ __forceinline__ void build_tables(uint32_t* lds, const GfJob& J, int nin, int nout) {
+  const int entries = nin * 32;  // (input, half, nibble)
+  for (int e = threadIdx.x; e < entries; e += blockDim.x) {
+    const int i = e >> 5;
+    const int h = (e >> 4) & 1;
+    const uint32_t x = static_cast<uint32_t>(e & 15) << (4 * h);
+    uint32_t v = 0;
+    for (int j = 0; j < nout; ++j) v |= gf_mul_dev(J.coef[j][i], x) << (8 * j);
+    lds[e] = v;
+  }
+}
+
+// v_bfe_u32 x, off, 8 -- emitted directly: hipcc rewrites a constant-offset
+// extract into a shift + and, which costs one more VALU op per table lookup
+template <int OFF>
+__device__ __forceinline__ uint32_t byte_of(uint32_t x) {
+  if constexpr (OFF == 0) {
+    return x & 0xFFu;
+  } else if constexpr (OFF == 24) {
+    return x >> 24;
+  } else {
+    uint32_t r;
+    asm("v_bfe_u32 %0, %1, %2, 8" : "=v"(r) : "v"(x), "i"(OFF));
+    return r;
+  }
+}
+
+// a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96); gfx950 has no
+// v_xor3_b32 and hipcc does not form bitop3 from plain XORs
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  uint32_t r;
+  asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0x96" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+  return r;
+}
+
+// dword at byte offset `off` of the LDS image
+__device__ __forceinline__ uint32_t lds_at(const uint32_t* lds, uint32_t off) {
+  return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + off);
+}
+
+// gather byte j of a[0..3] into one dword
+__device__ __forceinline__ uint32_t gather_byte(uint32_t a0, uint32_t a1, uint32_t a2, uint32_t a3, int j) {
+  const uint32_t sel_lo = 0x0c0c0000u | (static_cast<uint32_t>(4 + j) << 8) | static_cast<uint32_t>(j);
+  const uint32_t sel_hi = 0x00000c0cu | (static_cast<uint32_t>(4 + j) << 24) | (static_cast<uint32_t>(j) << 16);
+  return __builtin_amdgcn_perm(a1, a0, sel_lo) | __builtin_amdgcn_perm(a3, a2, sel_hi);
+}
+
+// Global-address-space views of the cell pointers: loads and stores through
+// them are global_load/store (vmcnt only), not flat ones, which would also
+// count on lgkmcnt and make every LDS table wait drain the HBM prefetch.
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u g_cu4;
+typedef __attribute__((address_space(1))) v4u g_u4;
+
+// NOUT and ACC are compile-time so that every loop iteration issues a fixed
+// sequence of memory instructions (NIN prefetch loads, [NOUT accumulate
+// loads], NOUT stores): the compiler can then wait for exactly the loads it
+// needs with a counted vmcnt instead of vmcnt(0), which is what lets the next
+// position's loads stay in flight behind this position's arithmetic and
+// stores (vmcnt counts stores too on gfx9).
+template <int NIN>
+__device__ __forceinline__ void load_vec(v4u (&x)[NIN], g_cu4* const (&in)[NIN], size_t v) {
+#pragma unroll
+  for (int i = 0; i < NIN; ++i) x[i] = in[i][v];
+}
+
+// out[j][v] (^)= sum_i coef[j][i] * x[i] for one 16-B position of every cell
+template <int NIN, int NOUT, bool ACC>
+__device__ __forceinline__ void gf_mac_vec(const uint32_t* lds, const v4u (&x)[NIN], g_u4* const (&out)[NOUT],
+                                           size_t v, bool store) {
+  uint32_t acc[16];
+#pragma unroll
+  for (int b = 0; b < 16; ++b) acc[b] = 0;
+#pragma unroll
+  for (int i = 0; i < NIN; ++i) {
+    const uint32_t w[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      // byte b of lo4 / hi4 = 4 * (low / high nibble of byte b) = table offset
+      const uint32_t lo4 = (w[q] << 2) & 0x3C3C3C3Cu;
+      const uint32_t hi4 = (w[q] >> 2) & 0x3C3C3C3Cu;
+      const uint32_t ol[4] = {byte_of<0>(lo4), byte_of<8>(lo4), byte_of<16>(lo4), byte_of<24>(lo4)};
+      const uint32_t oh[4] = {byte_of<0>(hi4), byte_of<8>(hi4), byte_of<16>(hi4), byte_of<24>(hi4)};
+#pragma unroll
+      for (int b = 0; b < 4; ++b) {
+        acc[4 * q + b] = xor3(acc[4 * q + b], lds_at(lds, i * kTableBytes + ol[b]),
+                              lds_at(lds, i * kTableBytes + 64 + oh[b]));
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    v4u r;
+    r.x = gather_byte(acc[0], acc[1], acc[2], acc[3], j);
+    r.y = gather_byte(acc[4], acc[5], acc[6], acc[7], j);
+    r.z = gather_byte(acc[8], acc[9], acc[10], acc[11], j);
+    r.w = gather_byte(acc[12], acc[13], acc[14], acc[15], j);
+    if constexpr (ACC) {
+      if (store) out[j][v] = r ^ out[j][v];
+    } else {
+      out[j][v] = r;
+    }
+  }
+}
+
+template <int NIN, bool ACC>
+__device__ __forceinline__ void xor_vec(const v4u (&x)[NIN], g_u4* out, size_t v, bool store) {
+  v4u r = x[0];
+#pragma unroll
+  for (int i = 1; i < NIN; ++i) r ^= x[i];
+  if constexpr (ACC) {
+    if (store) out[v] = r ^ out[v];
+  } else {
+    out[v] = r;
+  }
+}
+
+// The vector sweep shared by gf_mac and xor_reduce. The job's blocks sweep
+// its cells together, block-interleaved: at any moment they cover one
+// contiguous window of every cell, which keeps HBM row locality across the
+// ~100 concurrent cell streams (+8% over one contiguous range per block,
+// tools/gfbench.hip "GS").
+//
+// Software pipeline, unrolled by two over ping-pong register sets: the next
+// position's NIN loads are issued before this position's arithmetic and
+// stores, and nothing copies registers between the sets, so the compiler
+// waits for exactly the older loads (a counted vmcnt) and the prefetch stays
+// in flight behind the stores (gfx9's vmcnt counts stores too). Every lane
+// runs the same scalar trip count; positions past the end work on the last
+// vector instead (clamped loads, and a store of the value that position
+// already holds), so each iteration issues a fixed instruction sequence, the
+// waits can count the stores, and the body is emitted only twice. Bodies get
+// (position, in_range); only an accumulating body must skip out-of-range
+// stores, since re-applying its XOR would not be idempotent.
+template <int NIN, typename Body>
+__device__ __forceinline__ void sweep(g_cu4* const (&in)[NIN], size_t nvec, size_t vstep, int part, Body body) {
+  const size_t last = nvec - 1;
+  const size_t pairs = (nvec + 2 * vstep - 1) / (2 * vstep);
+  size_t v = static_cast<size_t>(part) * kBlock + threadIdx.x;
+  v4u xa[NIN], xb[NIN];
+  load_vec<NIN>(xa, in, v < nvec ? v : last);
+  for (size_t k = 0; k < pairs; ++k) {
+    const size_t vb = v + vstep;
+    load_vec<NIN>(xb, in, vb < nvec ? vb : last);
+    // keep the prefetch ahead of the arithmetic that waits on xa
+    __builtin_amdgcn_sched_barrier(0);
+    body(xa, v < nvec ? v : last, v < nvec);
+    const size_t va = vb + vstep;
+    load_vec<NIN>(xa, in, va < nvec ? va : last);
+    __builtin_amdgcn_sched_barrier(0);
+    body(xb, vb < nvec ? vb : last, vb < nvec);
+    v = va;
+  }
+}
+
+template <int NIN, int NOUT, bool ACC>
+__device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, int part) {
+  // static (not extern) so the table offsets fold into ds_read's immediate
+  __shared__ uint32_t lds[kMaxIn * kTableBytes / 4];
+
+  build_tables(lds, J, NIN, NOUT);
+  __syncthreads();
+
+  const size_t nvec = L.bytes_only ? 0 : L.nbytes / 16;
+  const size_t vstep = static_cast<size_t>(L.blocks_per_job) * kBlock;
+  if (nvec > 0) {
+    g_cu4* in[NIN];
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (J.in[i]);
+    g_u4* out[NOUT];
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) out[j] = (g_u4*) (J.out[j]);
+    sweep<NIN>(in, nvec, vstep, part,
+               [&](const v4u (&x)[NIN], size_t v, bool st) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, st); });
+  }
+
+  // byte path: the tail after the last whole 16-B vector, or everything when
+  // some pointer is not 16-B aligned; spread over the job's blocks
+  const size_t tail0 = nvec * 16;
+  for (size_t k = tail0 + static_cast<size_t>(part) * kBlock + threadIdx.x; k < L.nbytes; k += vstep) {
+    uint32_t acc = 0;
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) {
+      const uint32_t b = J.in[i][k];
+      acc ^= lds[i * 32 + (b & 15u)] ^ lds[i * 32 + 16 + (b >> 4)];
+    }
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) {
+      uint8_t r = static_cast<uint8_t>(acc >> (8 * j));
+      if constexpr (ACC) r ^= J.out[j][k];
+      J.out[j][k] = r;
+    }
+  }
+}
+
+template <int NIN, bool ACC>
+__device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, int part) {
+  const size_t nvec = L.bytes_only ? 0 : L.nbytes / 16;
+  const size_t vstep = static_cast<size_t>(L.blocks_per_job) * kBlock;
+  if (nvec > 0) {
+    g_cu4* in[NIN];
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (J.in[i]);
+    g_u4* out = (g_u4*) (J.out);
+    sweep<NIN>(in, nvec, vstep, part,
+               [&](const v4u (&x)[NIN], size_t v, bool st) { xor_vec<NIN, ACC>(x, out, v, st); });
+  }
+  const size_t tail0 = nvec * 16;
+  for (size_t k = tail0 + static_cast<size_t>(part) * kBlock + threadIdx.x; k < L.nbytes; k += vstep) {
+    uint8_t r = ACC ? J.out[k] : 0;
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) r ^= J.in[i][k];
+    J.out[k] = r;
+  }
+}
+
+// entry points: jobs from a device array (plans), or one job passed by
+// value in the kernel arguments (stripe primitives, no device descriptor)
+template <int NIN, int NOUT, bool ACC>
+__global__ void __launch_bounds__(kBlock) gf_mac_kernel(GfLaunch L) {
+  const int job = blockIdx.x / L.blocks_per_job;
+  gf_mac_body<NIN, NOUT, ACC>(L, L.jobs[job], blockIdx.x - job * L.blocks_per_job);
+}
+
+template <int NIN, int NOUT, bool ACC>
+__global__ void __launch_bounds__(kBlock) gf_mac_kernel_arg(GfLaunch L, GfJob J) {
+  gf_mac_body<NIN, NOUT, ACC>(L, J, blockIdx.x);
+}
+
+template <int NIN, bool ACC>
+__global__ void __launch_bounds__(kBlock) xor_kernel(XorLaunch L) {
+  const int job = blockIdx.x / L.blocks_per_job;
+  xor_body<NIN, ACC>(L, L.jobs[job], blockIdx.x - job * L.blocks_per_job);
+}
+
+template <int NIN, bool ACC>
+__global__ void __launch_bounds__(kBlock) xor_kernel_arg(XorLaunch L, XorJob J) {
+  xor_body<NIN, ACC>(L, J, blockIdx.x);
+}
+
+template <int N>
+constexpr KernelSet make_kernel_set() {
+  return KernelSet{
+      {{&gf_mac_kernel<N, 1, false>, &gf_mac_kernel<N, 1, true>},
+       {&gf_mac_kernel<N, 2, false>, &gf_mac_kernel<N, 2, true>},
+       {&gf_mac_kernel<N, 3, false>, &gf_mac_kernel<N, 3, true>},
+       {&gf_mac_kernel<N, 4, false>, &gf_mac_kernel<N, 4, true>}},
+      {{&gf_mac_kernel_arg<N, 1, false>, &gf_mac_kernel_arg<N, 1, true>},
+       {&gf_mac_kernel_arg<N, 2, false>, &gf_mac_kernel_arg<N, 2, true>},
+       {&gf_mac_kernel_arg<N, 3, false>, &gf_mac_kernel_arg<N, 3, true>},
+       {&gf_mac_kernel_arg<N, 4, false>, &gf_mac_kernel_arg<N, 4, true>}},
+      {&xor_kernel<N, false>, &xor_kernel<N, true>},
+      {&xor_kernel_arg<N, false>, &xor_kernel_arg<N, true>},
+  };
+}
+
+}  // namespace
+
+}  // namespace redset_hip
+
+// Defines `const KernelSet* FN(int nin)` for the listed input counts
+// (consecutive, starting at FIRST), nullptr for any other count.
+#define REDSET_DEFINE_KERNEL_SETS(FN, FIRST, ...)                                  \
+  namespace redset_hip {                                                           \
+  const KernelSet* FN(int nin) {                                                   \
+    static const KernelSet sets[] = {__VA_ARGS__};                                 \
+    const int n = static_cast<int>(sizeof(sets) / sizeof(sets[0]));                \
+    return (nin >= FIRST && nin < FIRST + n) ? &sets[nin - FIRST] : nullptr;       \
+  }                                                                                \
+  }

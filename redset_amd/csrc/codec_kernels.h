@@ -63,4 +63,17 @@ int gf_blocks_per_cu(int nin);
 
 constexpr int kBlock = 256;
 
+// The kernels of one input count: [nout - 1][accumulate] for gf_mac,
+// [accumulate] for xor_reduce; *_arg take the job by value.
+using GfKernel = void (*)(GfLaunch);
+using XorKernel = void (*)(XorLaunch);
+using GfKernelArg = void (*)(GfLaunch, GfJob);
+using XorKernelArg = void (*)(XorLaunch, XorJob);
+struct KernelSet {
+  GfKernel gf[kMaxOut][2];
+  GfKernelArg gf_arg[kMaxOut][2];
+  XorKernel xr[2];
+  XorKernelArg xr_arg[2];
+};
+
 }  // namespace redset_hip

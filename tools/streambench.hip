@@ -1,0 +1,143 @@
+// streambench: HBM rate of multi-stream read/write patterns on one MI355X,
+// to find what limits the codec's 8-read / 3-write stripe pattern.
+// Every job reads NIN streams and writes NOUT streams of `n` bytes each
+// (out[o] = xor of the inputs ^ o), grid-stride within the job like gf_mac.
+// Build: hipcc -O3 --offload-arch=gfx950 -o tools/streambench tools/streambench.hip
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                    \
+  do {                                                                           \
+    hipError_t e_ = (x);                                                         \
+    if (e_ != hipSuccess) {                                                      \
+      fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_)); \
+      exit(1);                                                                   \
+    }                                                                            \
+  } while (0)
+
+struct Job {
+  const uint4* in[8];
+  uint4* out[4];
+};
+
+template <int NIN, int NOUT, int U>
+__global__ void __launch_bounds__(256) kstream(const Job* jobs, size_t nvec, int bpj, size_t omask) {
+  const Job& J = jobs[blockIdx.x / bpj];
+  const int part = blockIdx.x % bpj;
+  const size_t stride = (size_t) bpj * 256 * U;
+  for (size_t v = (size_t) part * 256 * U + threadIdx.x; v < nvec; v += stride) {
+    uint4 acc[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) acc[u] = make_uint4(0, 0, 0, 0);
+    uint4 x[NIN > 0 ? NIN : 1][U];
+#pragma unroll
+    for (int i = 0; i < NIN; ++i)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (v + u * 256 < nvec) x[i][u] = J.in[i][v + u * 256];
+#pragma unroll
+    for (int i = 0; i < NIN; ++i)
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        acc[u].x ^= x[i][u].x;
+        acc[u].y ^= x[i][u].y;
+        acc[u].z ^= x[i][u].z;
+        acc[u].w ^= x[i][u].w;
+      }
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o)
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+        if (v + u * 256 < nvec) {
+          uint4 r = acc[u];
+          r.x ^= o + (unsigned) v;
+          J.out[o][(v + u * 256) & omask] = r;
+        }
+    if constexpr (NOUT == 0) {
+      // keep the loads live without a store per iteration
+      if ((acc[0].x ^ acc[0].y ^ acc[0].z ^ acc[0].w) == 0x9e3779b9u && v == 7) J.out[0][0] = acc[0];
+    }
+  }
+}
+
+struct Arena {
+  char* base;
+  size_t size, used;
+  void* take(size_t n) {
+    size_t a = (used + 4095) & ~(size_t) 4095;
+    if (a + n > size) {
+      fprintf(stderr, "arena full\n");
+      exit(1);
+    }
+    used = a + n;
+    return base + a;
+  }
+};
+
+template <int NIN, int NOUT, int U>
+void run(const char* name, Arena& A, int njobs, size_t n, int bpc, int cus, size_t gap, size_t omask = ~(size_t) 0) {
+  A.used = 0;
+  std::vector<Job> h(njobs);
+  for (int j = 0; j < njobs; ++j) {
+    for (int i = 0; i < 8; ++i) h[j].in[i] = nullptr;
+    for (int o = 0; o < 4; ++o) h[j].out[o] = nullptr;
+    for (int i = 0; i < NIN; ++i) h[j].in[i] = (const uint4*) A.take(n + gap);
+    for (int o = 0; o < (NOUT > 0 ? NOUT : 1); ++o) h[j].out[o] = (uint4*) A.take(n + gap);
+  }
+  Job* d;
+  CK(hipMalloc(&d, sizeof(Job) * njobs));
+  CK(hipMemcpy(d, h.data(), sizeof(Job) * njobs, hipMemcpyHostToDevice));
+  size_t nvec = n / 16;
+  int total = bpc * cus;
+  int bpj = total / njobs;
+  if (bpj < 1) bpj = 1;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int w = 0; w < 3; ++w) kstream<NIN, NOUT, U><<<bpj * njobs, 256>>>(d, nvec, bpj, omask);
+  CK(hipDeviceSynchronize());
+  const int reps = 10;
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) kstream<NIN, NOUT, U><<<bpj * njobs, 256>>>(d, nvec, bpj, omask);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  double bytes = (double) njobs * (NIN + NOUT) * n;
+  printf("%-34s jobs=%3d in=%d out=%d U=%d bpc=%d gap=%6zu  %8.4f ms  %7.1f GB/s\n", name, njobs, NIN, NOUT, U, bpc,
+         gap, ms, bytes / ms / 1e6);
+  CK(hipFree(d));
+}
+
+int main(int argc, char** argv) {
+  int dev = 0;
+  hipDeviceProp_t prop;
+  CK(hipGetDeviceProperties(&prop, dev));
+  const int cus = prop.multiProcessorCount;
+  const size_t n = (size_t) 64 << 20;
+  Arena A;
+  A.size = (size_t) 12 << 30;
+  CK(hipMalloc(&A.base, A.size));
+  CK(hipMemset(A.base, 0x5a, A.size));
+  A.used = 0;
+  printf("device %s, %d CUs, stream %zu MiB\n", prop.gcnArchName, cus, n >> 20);
+  const size_t small = ((size_t) 1 << 20) / 16 - 1;  // 1 MiB window: stores stay in L2
+  for (int rep = 0; rep < 2; ++rep)
+    for (int bpc : {2, 4}) {
+      run<8, 0, 1>("8r0w", A, 11, n, bpc, cus, 0);
+      run<8, 1, 1>("8r1w", A, 11, n, bpc, cus, 0);
+      run<8, 2, 1>("8r2w", A, 11, n, bpc, cus, 0);
+      run<8, 3, 1>("8r3w", A, 11, n, bpc, cus, 0);
+      run<8, 4, 1>("8r4w", A, 11, n, bpc, cus, 0);
+      run<8, 1, 1>("8r1w stores into 1 MiB (L2)", A, 11, n, bpc, cus, 0, small);
+      run<8, 3, 1>("8r3w stores into 1 MiB (L2)", A, 11, n, bpc, cus, 0, small);
+      run<4, 3, 1>("4r3w", A, 22, n, bpc, cus, 0);
+      run<0, 3, 1>("0r3w", A, 11, n, bpc, cus, 0);
+    }
+  CK(hipFree(A.base));
+  return 0;
+}

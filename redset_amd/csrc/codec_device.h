@@ -28,6 +28,16 @@
 
 #include "codec_kernels.h"
 
+// 0 (default): plain sweep -- load a position of every input, wait,
+// combine, store. 1: the software-pipelined sweep below. Measured A/B on one
+// box (bench.py RS(8+3), tools/ab_bench.sh, profiles/r01_ab_pipeline.txt):
+// plain 5.02 TB/s at 2 blocks/CU, pipelined 4.82; the HBM side prefers fewer
+// requests in flight (2 blocks/CU beat 3 and 4 for both), so the extra
+// prefetch only adds DRAM row contention.
+#ifndef REDSET_PIPELINE
+#define REDSET_PIPELINE 0
+#endif
+
 namespace redset_hip {
 
 namespace {
@@ -182,13 +192,30 @@ __device__ __forceinline__ void xor_vec(const v4u (&x)[NIN], g_u4* out, size_t v
 // waits can count the stores, and the body is emitted only twice. Bodies get
 // (position, in_range); only an accumulating body must skip out-of-range
 // stores, since re-applying its XOR would not be idempotent.
-template <int NIN, typename Body>
-__device__ __forceinline__ void sweep(g_cu4* const (&in)[NIN], size_t nvec, size_t vstep, int part, Body body) {
+//
+// `prime(position)` runs once after the first loads: a non-accumulating body
+// stores zeros to the position its first step will overwrite, so the loop is
+// entered with the same loads-then-stores sequence in flight as on the back
+// edge and the compiler's waits in the first half count the stores too.
+template <int NIN, typename Body, typename Prime>
+__device__ __forceinline__ void sweep(g_cu4* const (&in)[NIN], size_t nvec, size_t vstep, int part, Body body,
+                                      Prime prime) {
+#if !REDSET_PIPELINE
+  // plain sweep: load, wait, combine, store
+  (void) prime;
+  for (size_t v = static_cast<size_t>(part) * kBlock + threadIdx.x; v < nvec; v += vstep) {
+    v4u x[NIN];
+    load_vec<NIN>(x, in, v);
+    body(x, v, true);
+  }
+  return;
+#endif
   const size_t last = nvec - 1;
   const size_t pairs = (nvec + 2 * vstep - 1) / (2 * vstep);
   size_t v = static_cast<size_t>(part) * kBlock + threadIdx.x;
   v4u xa[NIN], xb[NIN];
   load_vec<NIN>(xa, in, v < nvec ? v : last);
+  prime(v < nvec ? v : last);
   for (size_t k = 0; k < pairs; ++k) {
     const size_t vb = v + vstep;
     load_vec<NIN>(xb, in, vb < nvec ? vb : last);
@@ -220,8 +247,15 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
     g_u4* out[NOUT];
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) out[j] = (g_u4*) (J.out[j]);
-    sweep<NIN>(in, nvec, vstep, part,
-               [&](const v4u (&x)[NIN], size_t v, bool st) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, st); });
+    sweep<NIN>(
+        in, nvec, vstep, part,
+        [&](const v4u (&x)[NIN], size_t v, bool st) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, st); },
+        [&](size_t v) {
+          if constexpr (!ACC) {
+#pragma unroll
+            for (int j = 0; j < NOUT; ++j) out[j][v] = v4u{0, 0, 0, 0};
+          }
+        });
   }
 
   // byte path: the tail after the last whole 16-B vector, or everything when
@@ -252,8 +286,11 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
 #pragma unroll
     for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (J.in[i]);
     g_u4* out = (g_u4*) (J.out);
-    sweep<NIN>(in, nvec, vstep, part,
-               [&](const v4u (&x)[NIN], size_t v, bool st) { xor_vec<NIN, ACC>(x, out, v, st); });
+    sweep<NIN>(
+        in, nvec, vstep, part, [&](const v4u (&x)[NIN], size_t v, bool st) { xor_vec<NIN, ACC>(x, out, v, st); },
+        [&](size_t v) {
+          if constexpr (!ACC) out[v] = v4u{0, 0, 0, 0};
+        });
   }
   const size_t tail0 = nvec * 16;
   for (size_t k = tail0 + static_cast<size_t>(part) * kBlock + threadIdx.x; k < L.nbytes; k += vstep) {

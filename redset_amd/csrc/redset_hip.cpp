@@ -51,17 +51,17 @@ int hip_check(hipError_t e, const char* what) {
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // Resident 256-thread blocks per CU the codec aims for. HBM streams best at
-// moderate occupancy here: with the software-pipelined gf_mac, 4 blocks
-// (16 waves) per CU beat 2, 3 and 8 (tools/gfbench.hip "PIPE"; a plain copy
-// also prefers few blocks, tools/membench.hip); REDSET_HIP_BLOCKS_PER_CU
-// overrides it.
+// low occupancy here: 2 blocks (8 waves, 64 KiB of loads in flight) per CU
+// beat 1, 3, 4 and 8 on every box measured (tools/bpc_sweep.sh,
+// profiles/r01_ab_pipeline.txt; 1 block starves the channels, more add DRAM
+// row contention); REDSET_HIP_BLOCKS_PER_CU overrides it.
 int target_blocks_per_cu(int occupancy) {
   static int env = -1;
   if (env < 0) {
     const char* s = std::getenv("REDSET_HIP_BLOCKS_PER_CU");
     env = (s && std::atoi(s) > 0) ? std::atoi(s) : 0;
   }
-  const int want = env > 0 ? env : 4;
+  const int want = env > 0 ? env : 2;
   return std::max(1, std::min(want, occupancy));
 }
 

@@ -26,7 +26,7 @@ def per_kernel(d, counter):
                 if row.get("Counter_Name") != counter:
                     continue
                 name = row["Kernel_Name"]
-                m = re.search(r"(\w+<\d+>)", name) if "redset_hip" in name else None
+                m = re.search(r"(\w+<[^>]*>)", name) if "redset_hip" in name else None
                 key = m.group(1) if m else name[:60]
                 disp = row.get("Dispatch_Id") or row.get("Correlation_Id")
                 sums[key] = sums.get(key, 0.0) + float(row["Counter_Value"])

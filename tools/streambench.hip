@@ -121,6 +121,24 @@ int main(int argc, char** argv) {
   const size_t n = (size_t) 64 << 20;
   Arena A;
   A.size = (size_t) 12 << 30;
+  if (getenv("STREAMBENCH_ALLOC")) {
+    // allocation-to-allocation variance: fresh allocation per round, each
+    // timed twice; flags from the env (0 default, 4 = hipDeviceMallocContiguous)
+    const unsigned flags = (unsigned) atoi(getenv("STREAMBENCH_ALLOC"));
+    A.size = (size_t) 8 << 30;
+    for (int round = 0; round < 6; ++round) {
+      if (flags == 0) CK(hipMalloc(&A.base, A.size));
+      else CK(hipExtMallocWithFlags((void**) &A.base, A.size, flags));
+      CK(hipMemset(A.base, 0x5a, A.size));
+      char name[64];
+      snprintf(name, sizeof(name), "alloc %d flags %u", round, flags);
+      run<8, 3, 1>(name, A, 11, n, 2, cus, 0);
+      run<8, 3, 1>(name, A, 11, n, 2, cus, 0);
+      run<8, 0, 1>(name, A, 11, n, 2, cus, 0);
+      CK(hipFree(A.base));
+    }
+    return 0;
+  }
   CK(hipMalloc(&A.base, A.size));
   CK(hipMemset(A.base, 0x5a, A.size));
   A.used = 0;

@@ -23,9 +23,22 @@ struct Job {
   uint4* out[4];
 };
 
+// global (address space 1) views: global_load/store, never flat (flat ops
+// also count on lgkmcnt and would tie LDS waits to HBM traffic)
+typedef unsigned int v4u __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(1))) const v4u gcv4;
+typedef __attribute__((address_space(1))) v4u gv4;
+__device__ __forceinline__ uint4 gld(const uint4* p, size_t i) {
+  v4u t = ((gcv4*) p)[i];
+  return make_uint4(t.x, t.y, t.z, t.w);
+}
+__device__ __forceinline__ void gst(uint4* p, size_t i, uint4 r) {
+  ((gv4*) p)[i] = v4u{r.x, r.y, r.z, r.w};
+}
+
 template <int NIN, int NOUT, int U>
 __global__ void __launch_bounds__(256) kstream(const Job* jobs, size_t nvec, int bpj, size_t omask) {
-  const Job& J = jobs[blockIdx.x / bpj];
+  const Job J = jobs[blockIdx.x / bpj];  // by value: pointers stay in registers
   const int part = blockIdx.x % bpj;
   const size_t stride = (size_t) bpj * 256 * U;
   for (size_t v = (size_t) part * 256 * U + threadIdx.x; v < nvec; v += stride) {
@@ -37,7 +50,7 @@ __global__ void __launch_bounds__(256) kstream(const Job* jobs, size_t nvec, int
     for (int i = 0; i < NIN; ++i)
 #pragma unroll
       for (int u = 0; u < U; ++u)
-        if (v + u * 256 < nvec) x[i][u] = J.in[i][v + u * 256];
+        if (v + u * 256 < nvec) x[i][u] = gld(J.in[i], v + u * 256);
 #pragma unroll
     for (int i = 0; i < NIN; ++i)
 #pragma unroll
@@ -54,11 +67,54 @@ __global__ void __launch_bounds__(256) kstream(const Job* jobs, size_t nvec, int
         if (v + u * 256 < nvec) {
           uint4 r = acc[u];
           r.x ^= o + (unsigned) v;
-          J.out[o][(v + u * 256) & omask] = r;
+          gst(J.out[o], (v + u * 256) & omask, r);
         }
     if constexpr (NOUT == 0) {
       // keep the loads live without a store per iteration
       if ((acc[0].x ^ acc[0].y ^ acc[0].z ^ acc[0].w) == 0x9e3779b9u && v == 7) J.out[0][0] = acc[0];
+    }
+  }
+}
+
+// Split roles: waves 0-3 of a 512-thread block load + combine and hand the
+// results to waves 4-7 through a double-buffered LDS ring; only those store.
+// The loading waves then never wait on store acknowledgements (gfx9 vmcnt
+// counts stores too), and the barrier is a raw s_barrier (no vmcnt drain).
+template <int NIN, int NOUT>
+__global__ void __launch_bounds__(512) ksplit(const Job* jobs, size_t nvec, int bpj) {
+  __shared__ uint4 ring[2][NOUT][256];
+  const Job J = jobs[blockIdx.x / bpj];
+  const int part = blockIdx.x % bpj;
+  const int t = threadIdx.x & 255;
+  const bool loader = threadIdx.x < 256;
+  const size_t vstep = (size_t) bpj * 256;
+  const size_t T = (nvec + vstep - 1) / vstep;
+  size_t v = (size_t) part * 256 + t;
+  for (size_t k = 0; k < T; ++k, v += vstep) {
+    const int b = k & 1;
+    if (loader) {
+      uint4 acc = make_uint4(0, 0, 0, 0);
+      if (v < nvec) {
+        uint4 x[NIN];
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) x[i] = gld(J.in[i], v);
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) {
+          acc.x ^= x[i].x; acc.y ^= x[i].y; acc.z ^= x[i].z; acc.w ^= x[i].w;
+        }
+      }
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) {
+        uint4 r = acc;
+        r.x ^= o + (unsigned) v;
+        ring[b][o][t] = r;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0) only: LDS traffic done, vm untouched
+    __builtin_amdgcn_s_barrier();
+    if (!loader && v < nvec) {
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) gst(J.out[o], v, ring[b][o][t]);
     }
   }
 }
@@ -113,6 +169,42 @@ void run(const char* name, Arena& A, int njobs, size_t n, int bpc, int cus, size
   CK(hipFree(d));
 }
 
+template <int NIN, int NOUT>
+void run_split(const char* name, Arena& A, int njobs, size_t n, int bpc, int cus) {
+  A.used = 0;
+  std::vector<Job> h(njobs);
+  for (int j = 0; j < njobs; ++j) {
+    for (int i = 0; i < 8; ++i) h[j].in[i] = nullptr;
+    for (int o = 0; o < 4; ++o) h[j].out[o] = nullptr;
+    for (int i = 0; i < NIN; ++i) h[j].in[i] = (const uint4*) A.take(n);
+    for (int o = 0; o < (NOUT > 0 ? NOUT : 1); ++o) h[j].out[o] = (uint4*) A.take(n);
+  }
+  Job* d;
+  CK(hipMalloc(&d, sizeof(Job) * njobs));
+  CK(hipMemcpy(d, h.data(), sizeof(Job) * njobs, hipMemcpyHostToDevice));
+  size_t nvec = n / 16;
+  int bpj = bpc * cus / njobs;
+  if (bpj < 1) bpj = 1;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  constexpr int NO = NOUT > 0 ? NOUT : 1;
+  for (int w = 0; w < 3; ++w) ksplit<NIN, NO><<<bpj * njobs, 512>>>(d, nvec, bpj);
+  CK(hipDeviceSynchronize());
+  const int reps = 10;
+  CK(hipEventRecord(e0));
+  for (int r = 0; r < reps; ++r) ksplit<NIN, NO><<<bpj * njobs, 512>>>(d, nvec, bpj);
+  CK(hipEventRecord(e1));
+  CK(hipEventSynchronize(e1));
+  float ms;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+  ms /= reps;
+  double bytes = (double) njobs * (NIN + NOUT) * n;
+  printf("%-34s jobs=%3d in=%d out=%d bpc=%d  %8.4f ms  %7.1f GB/s\n", name, njobs, NIN, NOUT, bpc, ms,
+         bytes / ms / 1e6);
+  CK(hipFree(d));
+}
+
 int main(int argc, char** argv) {
   int dev = 0;
   hipDeviceProp_t prop;
@@ -143,6 +235,15 @@ int main(int argc, char** argv) {
   CK(hipMemset(A.base, 0x5a, A.size));
   A.used = 0;
   printf("device %s, %d CUs, stream %zu MiB\n", prop.gcnArchName, cus, n >> 20);
+  if (getenv("STREAMBENCH_SPLIT")) {
+    for (int rep = 0; rep < 2; ++rep)
+      for (int bpc : {1, 2}) {
+        run<8, 3, 1>("8r3w same waves (bpc = 256-thr)", A, 11, n, 2 * bpc, cus, 0);
+        run_split<8, 3>("8r3w split roles (bpc = 512-thr)", A, 11, n, bpc, cus);
+        run_split<8, 2>("8r2w split roles (bpc = 512-thr)", A, 11, n, bpc, cus);
+      }
+    return 0;
+  }
   const size_t small = ((size_t) 1 << 20) / 16 - 1;  // 1 MiB window: stores stay in L2
   for (int rep = 0; rep < 2; ++rep)
     for (int bpc : {2, 4}) {

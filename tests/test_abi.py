@@ -46,6 +46,27 @@ def test_library_exports_every_declared_symbol(hiplib):
     assert b"gfx950" in hiplib.load().redset_hip_version()
 
 
+def test_mpi_library_exports_every_declared_symbol(hiplib):
+    """include/redset_hip_mpi.h's per-rank backends are exported by
+    libredset_hip_mpi.so (built where MPICH is present, as in this image).
+    Checked with nm: dlopen would need libmpi on the loader path."""
+    import shutil
+    import subprocess
+
+    mpi_h = os.path.join(ROOT, "include", "redset_hip_mpi.h")
+    mpi_so = os.path.join(ROOT, "redset_amd", "lib", "libredset_hip_mpi.so")
+    if not os.path.exists(mpi_so) or not shutil.which("nm"):
+        pytest.skip("libredset_hip_mpi.so not built (no MPICH) or nm missing")
+    text = re.sub(r"/\*.*?\*/", "", open(mpi_h).read(), flags=re.S)
+    declared = sorted(set(re.findall(r"\b(redset_hip_\w+)\s*\(", text)))
+    assert declared == ["redset_hip_rs_decode_rank", "redset_hip_rs_encode_rank", "redset_hip_xor_decode_rank",
+                        "redset_hip_xor_encode_rank"]
+    out = subprocess.run(["nm", "-D", "--defined-only", mpi_so], capture_output=True, text=True, check=True).stdout
+    exported = set(line.split()[-1] for line in out.splitlines() if line.strip())
+    for name in declared:
+        assert name in exported, name
+
+
 def test_missing_library_fails_loudly(tmp_path):
     from redset_amd import _lib
 

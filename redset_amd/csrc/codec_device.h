@@ -37,6 +37,10 @@
 #ifndef REDSET_PIPELINE
 #define REDSET_PIPELINE 0
 #endif
+// 1: timing-only build with the GF arithmetic replaced by XOR (never shipped)
+#ifndef REDSET_MEMONLY
+#define REDSET_MEMONLY 0
+#endif
 
 namespace redset_hip {
 
@@ -128,6 +132,22 @@ __device__ __forceinline__ void load_vec(v4u (&x)[NIN], g_cu4* const (&in)[NIN],
 template <int NIN, int NOUT, bool ACC>
 __device__ __forceinline__ void gf_mac_vec(const uint32_t* lds, const v4u (&x)[NIN], g_u4* const (&out)[NOUT],
                                            size_t v, bool store) {
+#if REDSET_MEMONLY
+  // timing-only build (A/B of the arithmetic's cost): same loads and stores,
+  // XOR instead of GF products -- results are wrong by design
+  v4u m = x[0];
+#pragma unroll
+  for (int i = 1; i < NIN; ++i) m ^= x[i];
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    if constexpr (ACC) {
+      if (store) out[j][v] = m ^ out[j][v];
+    } else {
+      out[j][v] = m + j;
+    }
+  }
+  return;
+#endif
   uint32_t acc[16];
 #pragma unroll
   for (int b = 0; b < 16; ++b) acc[b] = 0;

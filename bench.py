@@ -46,6 +46,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port beside (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
     ap.add_argument("--sharded", type=int, default=1, help="N>1: also time the RCCL sharded-rebuild leg")
+    ap.add_argument("--dist-backend", default="nccl",
+                    help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
     return ap.parse_args()
 
@@ -133,7 +135,8 @@ def timed(step, steps, warmup, dist_on, before=None):
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if dist_on:
-        t = torch.tensor([elapsed], device="cuda", dtype=torch.float64)
+        on_gpu = dist.get_backend() == "nccl"
+        t = torch.tensor([elapsed], device="cuda" if on_gpu else "cpu", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
@@ -169,12 +172,16 @@ def main():
         if world == 1 and args.gpus > 1:
             print(json.dumps({"error": f"--gpus {args.gpus} needs torchrun with {args.gpus} processes"}))
             sys.exit(2)
-    torch.cuda.set_device(local_rank)
+    dev = local_rank % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(dev)
     dist_on = world > 1
     if dist_on:
         import torch.distributed as dist
 
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", dev))
+        else:
+            dist.init_process_group(args.dist_backend)
 
     import redset_amd
 
@@ -247,6 +254,10 @@ def main():
     k_enc = f"gf_mac_kernel<{d}, {min(e, 4)}, false>"
     k_reb = f"gf_mac_kernel<{d}, {min(len(lost), 4)}, false>"
     t_enc, t_reb = load_traffic(args.traffic_json, k_enc), load_traffic(args.traffic_json, k_reb)
+    # the PMC file is recorded on the default workload; a different set shape
+    # or chunk size has different bytes per launch, so it does not apply
+    if not (t_enc and t_reb and 0.5 < t_enc / eb < 2.0 and 0.5 < t_reb / rb < 2.0):
+        t_enc = t_reb = None
     traffic = (t_enc + t_reb) // 2 if (t_enc and t_reb) else None
     result["roofline"] = {
         "bound": "hbm",

@@ -119,6 +119,30 @@ __global__ void __launch_bounds__(512) ksplit(const Job* jobs, size_t nvec, int 
   }
 }
 
+// Interleaved cells: the NIN + NOUT cells of a job stored block-interleaved
+// at granularity G vectors (cell k's block b at ((b * ncell) + k) * G), so
+// one position of every cell of a stripe lies in one contiguous region.
+template <int NIN, int NOUT>
+__global__ void __launch_bounds__(256) kinter(uint4* const* bases, size_t nvec, int bpj, size_t G) {
+  constexpr int NC = NIN + NOUT;
+  const int job = blockIdx.x / bpj;
+  const int part = blockIdx.x % bpj;
+  const gcv4* base = (const gcv4*) bases[job];
+  gv4* wbase = (gv4*) bases[job];
+  const size_t stride = (size_t) bpj * 256;
+  for (size_t v = (size_t) part * 256 + threadIdx.x; v < nvec; v += stride) {
+    const size_t blk = v / G, off = v % G;
+    v4u x[NIN];
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) x[i] = base[(blk * NC + i) * G + off];
+    v4u acc = x[0];
+#pragma unroll
+    for (int i = 1; i < NIN; ++i) acc ^= x[i];
+#pragma unroll
+    for (int o = 0; o < NOUT; ++o) wbase[(blk * NC + NIN + o) * G + off] = acc + (unsigned) o;
+  }
+}
+
 struct Arena {
   char* base;
   size_t size, used;
@@ -235,6 +259,36 @@ int main(int argc, char** argv) {
   CK(hipMemset(A.base, 0x5a, A.size));
   A.used = 0;
   printf("device %s, %d CUs, stream %zu MiB\n", prop.gcnArchName, cus, n >> 20);
+  if (getenv("STREAMBENCH_INTER")) {
+    const int njobs = 11;
+    std::vector<uint4*> hb(njobs);
+    for (int j = 0; j < njobs; ++j) hb[j] = (uint4*) (A.base + (size_t) j * 11 * n);
+    uint4** db;
+    CK(hipMalloc(&db, sizeof(uint4*) * njobs));
+    CK(hipMemcpy(db, hb.data(), sizeof(uint4*) * njobs, hipMemcpyHostToDevice));
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    for (int rep = 0; rep < 2; ++rep) {
+      run<8, 3, 1>("8r3w separate cells", A, 11, n, 2, cus, 0);
+      for (size_t Gb : {(size_t) 1024, (size_t) 4096, (size_t) 16384, (size_t) 65536, (size_t) 1 << 20})
+        for (int bpc : {2, 4}) {
+          const size_t G = Gb / 16, nvec = n / 16;
+          const int bpj = bpc * cus / njobs;
+          for (int w = 0; w < 3; ++w) kinter<8, 3><<<bpj * njobs, 256>>>(db, nvec, bpj, G);
+          CK(hipDeviceSynchronize());
+          CK(hipEventRecord(e0));
+          for (int r = 0; r < 10; ++r) kinter<8, 3><<<bpj * njobs, 256>>>(db, nvec, bpj, G);
+          CK(hipEventRecord(e1));
+          CK(hipEventSynchronize(e1));
+          float ms;
+          CK(hipEventElapsedTime(&ms, e0, e1));
+          ms /= 10;
+          printf("8r3w interleaved G=%7zu B bpc=%d  %8.4f ms  %7.1f GB/s\n", Gb, bpc, ms, 11.0 * 11 * n / ms / 1e6);
+        }
+    }
+    return 0;
+  }
   if (getenv("STREAMBENCH_SPLIT")) {
     for (int rep = 0; rep < 2; ++rep)
       for (int bpc : {1, 2}) {

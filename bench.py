@@ -43,6 +43,9 @@ def parse():
     ap.add_argument("--encoding", type=int, default=3, help="parity cells per stripe e")
     ap.add_argument("--chunk-mib", type=float, default=64.0)
     ap.add_argument("--lost", default="1,2", help="members rebuilt each step")
+    ap.add_argument("--cell-pad-mib", type=float, default=16.0,
+                    help="MiB of padding after every cell in HBM: breaks the 2^26-byte aliasing of 64 MiB "
+                         "cells (+1-10%% depending on the box, profiles/r01_cell_placement.txt)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port beside (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
     ap.add_argument("--sharded", type=int, default=1, help="N>1: also time the RCCL sharded-rebuild leg")
@@ -194,7 +197,7 @@ def main():
 
     # this rank's own set, all cells resident in HBM
     codec = redset_amd.RSCodec(p, e)
-    lay = redset_amd.SetLayout.allocate(p, d, e, chunk)
+    lay = redset_amd.SetLayout.allocate(p, d, e, chunk, pad=int(args.cell_pad_mib * MIB))
     g = torch.Generator(device="cuda")
     g.manual_seed(1234 + rank)
     for r in range(p):
@@ -240,6 +243,7 @@ def main():
             "ranks": p,
             "encoding": e,
             "chunk_bytes": chunk,
+            "cell_stride_bytes": lay.cell_stride,
             "sets": world,
             "bytes_per_step_per_gpu": bytes_per_step,
             "parallelism": "single GPU" if world == 1 else f"{world} independent sets, one per GPU (no collective)",

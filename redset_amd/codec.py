@@ -214,10 +214,14 @@ class SetLayout:
     storage: object  # torch.uint8 tensor
 
     @classmethod
-    def allocate(cls, ranks: int, data_cells: int, parity_cells: int, chunk_size: int, device="cuda"):
+    def allocate(cls, ranks: int, data_cells: int, parity_cells: int, chunk_size: int, device="cuda",
+                 pad: int = 0):
+        """``pad`` extra bytes after every cell (rounded to CELL_ALIGN): moves
+        the cells of a stripe relative to each other in HBM."""
         import torch
 
         stride = max(CELL_ALIGN, -(-chunk_size // CELL_ALIGN) * CELL_ALIGN)
+        stride += -(-pad // CELL_ALIGN) * CELL_ALIGN
         per = (data_cells + parity_cells) * stride
         storage = torch.empty(ranks * per, dtype=torch.uint8, device=device)
         return cls(ranks, data_cells, parity_cells, chunk_size, stride, storage)

@@ -259,6 +259,38 @@ int main(int argc, char** argv) {
   CK(hipMemset(A.base, 0x5a, A.size));
   A.used = 0;
   printf("device %s, %d CUs, stream %zu MiB\n", prop.gcnArchName, cus, n >> 20);
+  if (getenv("STREAMBENCH_SLIDE")) {
+    // same layout (11 stripes x 11 cells of 64 MiB, 7.6 GiB) at different
+    // offsets inside one 40 GiB allocation: does the physical region matter?
+    CK(hipFree(A.base));
+    const size_t G = (size_t) 1 << 30;
+    char* big;
+    CK(hipMalloc(&big, 40 * G));
+    CK(hipMemset(big, 0x5a, 40 * G));
+    for (int rep = 0; rep < 2; ++rep)
+      for (size_t off = 0; off + 8 * G <= 40 * G; off += 4 * G) {
+        Arena B{big + off, 8 * G, 0};
+        char name[64];
+        snprintf(name, sizeof(name), "8r3w at +%zu GiB", off / G);
+        run<8, 3, 1>(name, B, 11, n, 2, cus, 0);
+      }
+    return 0;
+  }
+  if (getenv("STREAMBENCH_GAPS")) {
+    // separate cells with a pad after each: does the relative placement of a
+    // stripe's cells matter?
+    const size_t M = 1 << 20;
+    if (getenv("STREAMBENCH_BIG")) {
+      CK(hipFree(A.base));
+      A.size = (size_t) atoi(getenv("STREAMBENCH_BIG")) << 30;
+      CK(hipMalloc(&A.base, A.size));
+      CK(hipMemset(A.base, 0x5a, A.size));
+    }
+    for (int rep = 0; rep < 2; ++rep)
+      for (size_t gap : {(size_t) 0, 16 * M, 32 * M, 0 * M, 16 * M, 32 * M})
+        run<8, 3, 1>("8r3w cells + gap", A, 11, n, 2, cus, gap);
+    return 0;
+  }
   if (getenv("STREAMBENCH_INTER")) {
     const int njobs = 11;
     std::vector<uint4*> hb(njobs);

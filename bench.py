@@ -49,6 +49,7 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port beside (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
     ap.add_argument("--sharded", type=int, default=1, help="N>1: also time the RCCL sharded-rebuild leg")
+    ap.add_argument("--xor", type=int, default=1, help="also time the XOR set of configs[1] (rank 0)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -143,6 +144,52 @@ def timed(step, steps, warmup, dist_on, before=None):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
     return elapsed
+
+
+def xor_leg(args, chunk, stream):
+    """BASELINE.json configs[1]: XOR set of 8 ranks, 64 MiB chunks -- encode
+    all 8 parity cells + rebuild one member (xor_kernel<7>), timed with HIP
+    events on the launch stream; reported beside the RS line."""
+    import torch
+    import redset_amd
+
+    p = 8
+    lay = redset_amd.SetLayout.allocate(p, p - 1, 1, chunk, pad=int(args.cell_pad_mib * MIB))
+    g = torch.Generator(device="cuda")
+    g.manual_seed(77)
+    for r in range(p):
+        n = lay.lofi(r).numel()
+        lay.lofi(r).copy_(torch.randint(0, 256, (n,), dtype=torch.uint8, device="cuda", generator=g))
+    enc = redset_amd.xor_plan_encode(p, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    reb = redset_amd.xor_plan_rebuild(p, 3, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    for _ in range(args.warmup):
+        enc.execute(stream)
+        reb.execute(stream)
+    t_enc = t_reb = 0.0
+    for _ in range(args.steps):
+        ev[0].record(stream)
+        enc.execute(stream)
+        ev[1].record(stream)
+        reb.execute(stream)
+        ev[2].record(stream)
+        torch.cuda.synchronize()
+        t_enc += ev[0].elapsed_time(ev[1])
+        t_reb += ev[1].elapsed_time(ev[2])
+    eb = enc.bytes_read + enc.bytes_written
+    rb = reb.bytes_read + reb.bytes_written
+    t_enc, t_reb = t_enc / args.steps, t_reb / args.steps
+    return {
+        "workload": f"XOR p={p}, chunk {chunk // MIB} MiB: encode all {p} parity cells + rebuild member 3 "
+                    "(BASELINE.json configs[1])",
+        "value": round((eb + rb) / ((t_enc + t_reb) * 1e-3) / 1e9, 1),
+        "unit": "GB/s",
+        "frac": round((eb + rb) / ((t_enc + t_reb) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+        "encode_GBps": round(eb / (t_enc * 1e-3) / 1e9, 1),
+        "rebuild_GBps": round(rb / (t_reb * 1e-3) / 1e9, 1),
+        "avg_launch_ms": {"encode": round(t_enc, 4), "rebuild": round(t_reb, 4)},
+        "algorithmic_bytes_per_launch": {"encode": eb, "rebuild": rb},
+    }
 
 
 def sharded_leg(args, p, e, chunk, lost, world, rank):
@@ -281,6 +328,8 @@ def main():
         "encode_read_GBps": round(enc_plan.bytes_read / (enc_ms * 1e-3) / 1e9, 1),
         "rebuild_GBps": round(rb / (reb_ms * 1e-3) / 1e9, 1),
     }
+    if args.xor and rank == 0:
+        result["xor"] = xor_leg(args, chunk, stream)
     if dist_on and args.sharded:
         # second leg: the multi-rank rebuild with its RCCL exchange. It must
         # not cost the main line: a failure is reported in "sharded" (every

@@ -14,10 +14,11 @@ independent objects, so the timed step shards them across ranks with no
 data-path collective: every GPU encodes + rebuilds its own set exactly as at
 N=1, and `value` = all ranks' algorithmic bytes / the max-over-ranks step
 time. The path's one real exchange -- the multi-rank rebuild whose chunks are
-gathered over xGMI -- is measured after it as a second timed
-leg and reported under "sharded": N sets whose members are spread round-robin
-over the GPUs, every stripe computed column-sharded over all GPUs after an
-RCCL all-to-all of cell slices (redset_amd.dist), exchange inside the timing.
+gathered over xGMI (BASELINE.json configs[3]) -- is measured
+after it as a second timed leg and reported under "sharded": N sets whose
+members are spread round-robin over the GPUs, erased members rebuilt
+column-sharded over all GPUs after an RCCL P2P gather of the decode inputs'
+slices (redset_amd.dist), exchange inside the timing, result checked bit-exact.
 
 Prints ONE JSON line on rank 0.
 """
@@ -146,6 +147,46 @@ def timed(step, steps, warmup, dist_on, before=None):
     return elapsed
 
 
+def round_trip(lay, enc_plan, reb_plan, lost, stream):
+    """Full-size encode -> erase -> rebuild: the erased members' cells (data
+    and the parity the encode just wrote) must come back bit for bit -- the
+    size-independent parity property of the timed workload (the oracle
+    comparisons themselves live in tests/ at sizes the CPU finishes)."""
+    import torch
+
+    enc_plan.execute(stream)
+    torch.cuda.synchronize()
+    cells = [c for r in lost for c in
+             [lay.data_cell(r, s) for s in range(lay.data_cells)] + [lay.parity_cell(r, i) for i in range(lay.parity_cells)]]
+    snap = [c.clone() for c in cells]
+    for c in cells:
+        c.fill_(0xEE)
+    reb_plan.execute(stream)
+    torch.cuda.synchronize()
+    return all(torch.equal(c, s) for c, s in zip(cells, snap))
+
+
+def copy_probe(stream, nbytes=1 << 30, reps=10):
+    """This box's HBM rate for a plain device-to-device copy (torch's copy
+    kernel, read + write bytes / time): boxes differ by several percent, so
+    the codec's rate is reported beside what the same HBM does for a copy."""
+    import torch
+
+    a = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    b = torch.empty_like(a)
+    a.fill_(1)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    with torch.cuda.stream(stream):
+        for _ in range(3):
+            b.copy_(a)
+        e0.record(stream)
+        for _ in range(reps):
+            b.copy_(a)
+        e1.record(stream)
+    torch.cuda.synchronize()
+    return round(2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+
+
 def xor_leg(args, chunk, stream):
     """BASELINE.json configs[1]: XOR set of 8 ranks, 64 MiB chunks -- encode
     all 8 parity cells + rebuild one member (xor_kernel<7>), timed with HIP
@@ -179,6 +220,7 @@ def xor_leg(args, chunk, stream):
     eb = enc.bytes_read + enc.bytes_written
     rb = reb.bytes_read + reb.bytes_written
     t_enc, t_reb = t_enc / args.steps, t_reb / args.steps
+    ok = round_trip(lay, enc, reb, [3], stream)
     return {
         "workload": f"XOR p={p}, chunk {chunk // MIB} MiB: encode all {p} parity cells + rebuild member 3 "
                     "(BASELINE.json configs[1])",
@@ -189,25 +231,42 @@ def xor_leg(args, chunk, stream):
         "rebuild_GBps": round(rb / (t_reb * 1e-3) / 1e9, 1),
         "avg_launch_ms": {"encode": round(t_enc, 4), "rebuild": round(t_reb, 4)},
         "algorithmic_bytes_per_launch": {"encode": eb, "rebuild": rb},
+        "round_trip_bit_exact": ok,
     }
 
 
 def sharded_leg(args, p, e, chunk, lost, world, rank):
-    """N sets spread over N GPUs, rebuilt column-sharded with RCCL exchanges
-    (redset_amd.dist), timed like the main step."""
+    """BASELINE.json configs[3]: erase members, rebuild them with the set's
+    cells spread over the node's GPUs (redset_amd.dist). N sets, member m on
+    GPU m mod N; the timed step is the rebuild only -- gather my column slice
+    of every decode input over RCCL, gf_mac, return the rebuilt slices to
+    their hosts. Parity comes from one untimed sharded encode beforehand.
+    After timing every GPU checks that its lost members' slabs are back bit
+    for bit (min over ranks)."""
+    import torch
+    import torch.distributed as dist
     from redset_amd import dist as rdist
 
     runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank)
-    s_elapsed = timed(lambda i: runner.step(), args.steps, args.warmup, True, before=runner.reset_timing)
+    runner.encode()
+    snap = runner.lost_snapshot()
+    runner.erase()
+    s_elapsed = timed(lambda i: runner.rebuild(), args.steps, args.warmup, True, before=runner.reset_timing)
     s_step = s_elapsed / args.steps
+    ok = torch.tensor([1 if runner.matches(snap) else 0], dtype=torch.int32,
+                      device="cuda" if dist.get_backend() == "nccl" else "cpu")
+    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    value = world * runner.algorithmic_bytes("rebuild") / s_step / 1e9
     out = {
-        "workload": (f"{world} sets of p={p}, members round-robin over {world} GPUs; encode + rebuild of "
-                     f"members {lost} of every set, column-sharded, RCCL all-to-all + batched P2P"),
-        "value": round(world * runner.algorithmic_bytes / s_step / 1e9, 2),
+        "workload": (f"{world} sets of p={p} (RS({p - e}+{e}), chunk {chunk >> 20} MiB), members round-robin over "
+                     f"{world} GPUs; rebuild of members {lost} of every set, column-sharded (BASELINE.json configs[3])"),
+        "value": round(value, 2),
         "unit": "GB/s",
+        "frac": round(value / world / HBM_PEAK_GBPS, 4),
         "ms_per_step": round(s_step * 1e3, 4),
+        "bit_exact": bool(ok.item()),
     }
-    out.update(runner.report(s_step))
+    out.update(runner.report(s_step, "rebuild"))
     return out
 
 
@@ -269,6 +328,13 @@ def main():
 
     elapsed = timed(step, args.steps, args.warmup, dist_on)
     ms_per_step = elapsed * 1e3 / args.steps
+    # after the timed region: the round trip on this rank's set, and the box's copy rate
+    rt_ok = round_trip(lay, enc_plan, reb_plan, lost, stream)
+    if dist_on:
+        flag = torch.tensor([int(rt_ok)], dtype=torch.int32, device="cuda" if args.dist_backend == "nccl" else "cpu")
+        dist.all_reduce(flag, op=dist.ReduceOp.MIN)
+        rt_ok = bool(flag.item())
+    box_copy = copy_probe(stream)
     value = world * bytes_per_step / (elapsed / args.steps) / 1e9
 
     result = {
@@ -327,6 +393,12 @@ def main():
         "encode_GBps": round(eb / (enc_ms * 1e-3) / 1e9, 1),
         "encode_read_GBps": round(enc_plan.bytes_read / (enc_ms * 1e-3) / 1e9, 1),
         "rebuild_GBps": round(rb / (reb_ms * 1e-3) / 1e9, 1),
+    }
+    result["round_trip_bit_exact"] = rt_ok
+    result["box_reference"] = {
+        "torch_copy_GBps": box_copy,
+        "codec_vs_copy": round(achieved / box_copy, 4),
+        "note": "same box, same process: device-to-device copy of 1 GiB (read + write bytes)",
     }
     if args.xor and rank == 0:
         result["xor"] = xor_leg(args, chunk, stream)

@@ -27,8 +27,9 @@ backend is the HIP library.
 from __future__ import annotations
 
 from dataclasses import dataclass
-from typing import Callable, List, Sequence
+from typing import Callable, Dict, List, Sequence, Tuple
 
+import numpy as np
 import torch
 import torch.distributed as dist
 
@@ -62,6 +63,51 @@ class HipBackend:
         return lambda: plan.execute()
 
 
+def rebuild_inputs(p: int, e: int, lost: Sequence[int]) -> Tuple[np.ndarray, np.ndarray]:
+    """Which cells of each surviving member some stripe's decode reads.
+
+    Returns (data[p][d], parity[p][e]) boolean masks. A stripe's decode
+    (redset_rs_reduce_decode + redset_rs_gaussian_solve as one linear map,
+    redset_hip_rs_decode_matrix) reads the stripe's surviving data cells and
+    the parity rows redset_rs_gaussian_solve_identify_rows selects
+    (src/redset_reedsolomon_common.c:425-564); the parity rows it leaves out
+    never have to cross the fabric. Member s's cell in stripe c is data cell
+    get_data_id(s, c) when get_encoding_id(s, c) < p, else parity slot
+    get_encoding_id(s, c) - p (src/redset_reedsolomon_common.c:822-853)."""
+    from .codec import RSCodec
+
+    d = p - e
+    need_d = np.zeros((p, d), dtype=bool)
+    need_p = np.zeros((p, e), dtype=bool)
+    if not lost:
+        return need_d, need_p
+    codec = RSCodec(p, e)
+    for c in range(p):
+        M = codec.decode_matrix(list(lost), c)
+        for s in range(p):
+            if s in lost or not M[:, s].any():
+                continue
+            enc = codec.encoding_id(s, c)
+            if enc < p:
+                need_d[s, codec.data_id(s, c)] = True
+            else:
+                need_p[s, enc - p] = True
+    codec.close()
+    return need_d, need_p
+
+
+def _runs(flags: Sequence[bool]) -> List[Tuple[int, int]]:
+    """[a, b) index ranges of the True entries"""
+    out, a = [], None
+    for i, f in enumerate(list(flags) + [False]):
+        if f and a is None:
+            a = i
+        elif not f and a is not None:
+            out.append((a, i))
+            a = None
+    return out
+
+
 class ShardedSetRunner:
     """Encode + rebuild of `world` sets column-sharded over `world` ranks."""
 
@@ -74,11 +120,13 @@ class ShardedSetRunner:
         W = -(-chunk // world)
         self.W = -(-W // SLICE_ALIGN) * SLICE_ALIGN
         # bytes of my column slice of each cell (the last slice may be short)
-        self.my_len = max(0, min(chunk, (rank + 1) * self.W) - rank * self.W)
+        self.my_len = self.slice_len(rank)
         self.backend = backend if backend is not None else HipBackend(p, e)
         self._place()
         self.timing = self.device.type == "cuda"
         self._events = []
+        self._gather_ops = None
+        self._return_ops = None
         d, W, ph = self.d, self.W, p  # every GPU hosts p members
         u8 = dict(dtype=torch.uint8, device=self.device)
         self.D_host = torch.zeros(world, ph, d, W, **u8)
@@ -105,6 +153,7 @@ class ShardedSetRunner:
         so an exchange can skip them with contiguous views."""
         self._where = {}
         self.n_alive = []
+        self._hosted = []
         for g in range(self.world):
             mine = [m for m in range(self.world * self.p) if m % self.world == g]
             alive = [m for m in mine if (m % self.p) not in self.lost]
@@ -112,6 +161,7 @@ class ShardedSetRunner:
             for j, m in enumerate(alive + dead):
                 self._where[m] = (g, j)
             self.n_alive.append(len(alive))
+            self._hosted.append(alive + dead)
 
     def host_of(self, k: int, r: int):
         """(GPU, hosted index) of member r of set k."""
@@ -126,26 +176,62 @@ class ShardedSetRunner:
         return SetViews(lofi, parity)
 
     # ---- exchanges -------------------------------------------------------
-    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor, skip_lost: bool = False) -> None:
-        """out[h] <- inp[me] of rank h, for every h. With skip_lost, the lost
-        members (hosted last, see host_of) are not sent: their cells are gone."""
+    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor) -> None:
+        """out[h] <- inp[me] of rank h, for every h (encode: every cell)."""
         if self.world == 1:
             out.copy_(inp)
             return
-        if not skip_lost or not self.lost:
-            dist.all_to_all_single(out, inp)
-            return
-        # uneven all-to-all as one batch of P2P ops (gloo has no uneven
-        # all_to_all; RCCL groups the batch into one launch)
-        me, n_send = self.rank, self.n_alive[self.rank]
-        out[me, :n_send].copy_(inp[me, :n_send])
-        ops = []
+        dist.all_to_all_single(out, inp)
+
+    def _build_rebuild_gather(self) -> None:
+        """The rebuild's gather as one batch of P2P ops: my column slice of
+        every cell some decode reads (rebuild_inputs), from every survivor's
+        host. Lost members are hosted last and never sent; parity rows no
+        decode selects stay home. Cells are flattened per GPU as
+        (hosted member, cell), so neighbouring needed cells merge into one op."""
+        p, d, e, W, me = self.p, self.d, self.e, self.W, self.rank
+        need_d, need_p = rebuild_inputs(p, e, self.lost)
+
+        def runs(h):
+            alive = self._hosted[h][:self.n_alive[h]]
+            fd = [bool(need_d[m % p, s]) for m in alive for s in range(d)]
+            fp = [bool(need_p[m % p, i]) for m in alive for i in range(e)]
+            return _runs(fd), _runs(fp)
+
+        def rows(t, g):  # GPU g's slab of t as [hosted member * cell, W]
+            return t[g].view(-1, W)
+
+        self._gather_local = []
+        self._gather_ops = []
+        self._gather_sent = 0
+        my_d, my_p = runs(me)
+        for a, b in my_d:
+            self._gather_local.append((rows(self.D_gath, me)[a:b], rows(self.D_host, me)[a:b]))
+        for a, b in my_p:
+            self._gather_local.append((rows(self.P_gath, me)[a:b], rows(self.P_host, me)[a:b]))
         for g in range(self.world):
-            if g != me:
-                ops.append(dist.P2POp(dist.isend, inp[g, :n_send], g))
-                ops.append(dist.P2POp(dist.irecv, out[g, :self.n_alive[g]], g))
-        for req in dist.batch_isend_irecv(ops):
-            req.wait()
+            if g == me:
+                continue
+            for a, b in my_d:
+                self._gather_ops.append(dist.P2POp(dist.isend, rows(self.D_host, g)[a:b], g))
+                self._gather_sent += (b - a) * W
+            for a, b in my_p:
+                self._gather_ops.append(dist.P2POp(dist.isend, rows(self.P_host, g)[a:b], g))
+                self._gather_sent += (b - a) * W
+            their_d, their_p = runs(g)
+            for a, b in their_d:
+                self._gather_ops.append(dist.P2POp(dist.irecv, rows(self.D_gath, g)[a:b], g))
+            for a, b in their_p:
+                self._gather_ops.append(dist.P2POp(dist.irecv, rows(self.P_gath, g)[a:b], g))
+
+    def _gather_rebuild_inputs(self) -> None:
+        if self._gather_ops is None:
+            self._build_rebuild_gather()
+        for dst, src in self._gather_local:
+            dst.copy_(src)
+        if self._gather_ops:
+            for req in dist.batch_isend_irecv(self._gather_ops):
+                req.wait()
 
     def _mark(self, name: str) -> None:
         if self.timing:
@@ -153,26 +239,33 @@ class ShardedSetRunner:
             ev.record()
             self._events.append((name, ev))
 
-    def _return_lost(self) -> None:
-        """Send rebuilt slices of lost members to their hosts (the reference's
-        gather to the failed ranks, src/redset_reedsolomon.c:713-733)."""
-        ops = []
+    def _build_return(self) -> None:
+        """Rebuilt slices of lost members go to their hosts (the reference's
+        gather to the failed ranks, src/redset_reedsolomon.c:713-733): my own
+        slice is a local copy, the others arrive from their peers."""
+        self._return_local, self._return_ops, self._return_sent = [], [], 0
         for k in range(self.world):
             for r in self.lost:
                 h, j = self.host_of(k, r)
                 if h == self.rank:
-                    # my own slice: local copy; other slices arrive from peers
-                    self.D_host[self.rank, j].copy_(self.D_gath[h, j])
-                    self.P_host[self.rank, j].copy_(self.P_gath[h, j])
+                    self._return_local.append((self.D_host[self.rank, j], self.D_gath[h, j]))
+                    self._return_local.append((self.P_host[self.rank, j], self.P_gath[h, j]))
                     for g in range(self.world):
                         if g != self.rank:
-                            ops.append(dist.P2POp(dist.irecv, self.D_host[g, j], g))
-                            ops.append(dist.P2POp(dist.irecv, self.P_host[g, j], g))
+                            self._return_ops.append(dist.P2POp(dist.irecv, self.D_host[g, j], g))
+                            self._return_ops.append(dist.P2POp(dist.irecv, self.P_host[g, j], g))
                 else:
-                    ops.append(dist.P2POp(dist.isend, self.D_gath[h, j], h))
-                    ops.append(dist.P2POp(dist.isend, self.P_gath[h, j], h))
-        if ops:
-            for req in dist.batch_isend_irecv(ops):
+                    self._return_ops.append(dist.P2POp(dist.isend, self.D_gath[h, j], h))
+                    self._return_ops.append(dist.P2POp(dist.isend, self.P_gath[h, j], h))
+                    self._return_sent += self.D_gath[h, j].numel() + self.P_gath[h, j].numel()
+
+    def _return_lost(self) -> None:
+        if self._return_ops is None:
+            self._build_return()
+        for dst, src in self._return_local:
+            dst.copy_(src)
+        if self._return_ops:
+            for req in dist.batch_isend_irecv(self._return_ops):
                 req.wait()
 
     # ---- operations ------------------------------------------------------
@@ -200,8 +293,7 @@ class ShardedSetRunner:
     def rebuild(self) -> None:
         """Rebuild the lost members of every set from the survivors."""
         self._mark("rebuild_start")
-        self._all_to_all(self.D_gath, self.D_host, skip_lost=True)
-        self._all_to_all(self.P_gath, self.P_host, skip_lost=True)
+        self._gather_rebuild_inputs()
         self._mark("rebuild_gathered")
         for fn in self._rebuild:
             fn()
@@ -213,24 +305,53 @@ class ShardedSetRunner:
         self.encode()
         self.rebuild()
 
-    # ---- accounting ------------------------------------------------------
-    @property
-    def algorithmic_bytes(self) -> int:
-        """Per-GPU algorithmic bytes of one step (one set's worth: encode
-        (d+e)*C per stripe + rebuild (d+m)*C per stripe, p stripes)."""
-        p, d, e, m, C = self.p, self.d, self.e, len(self.lost), self.chunk
-        return p * (d + e) * C + (p * (d + m) * C if m else 0)
+    # ---- verification --------------------------------------------------
+    def lost_snapshot(self) -> List[Tuple[int, torch.Tensor, torch.Tensor]]:
+        """Copies of this GPU's hosted slabs of the members `erase` destroys."""
+        snap = []
+        for k in range(self.world):
+            for r in self.lost:
+                h, j = self.host_of(k, r)
+                if h == self.rank:
+                    snap.append((j, self.D_host[:, j].clone(), self.P_host[:, j].clone()))
+        return snap
 
-    @property
-    def exchanged_bytes(self) -> int:
-        """Bytes this GPU sends per step over the fabric (average GPU)."""
+    def slice_len(self, g: int) -> int:
+        """Bytes of cell column slice g that are cell bytes (the rest of the
+        last slice's W is padding)."""
+        return max(0, min(self.chunk, (g + 1) * self.W) - g * self.W)
+
+    def matches(self, snap) -> bool:
+        """Every cell byte of the hosted slabs in `snap` is back, bit for bit."""
+        for j, dd, pp in snap:
+            for g in range(self.world):
+                n = self.slice_len(g)
+                if not (torch.equal(self.D_host[g, j, :, :n], dd[g, :, :n])
+                        and torch.equal(self.P_host[g, j, :, :n], pp[g, :, :n])):
+                    return False
+        return True
+
+    # ---- accounting ------------------------------------------------------
+    def algorithmic_bytes(self, op: str = "step") -> int:
+        """Per-GPU algorithmic bytes (one set's worth, p stripes): encode
+        (d+e)*C per stripe, rebuild (d+m)*C per stripe (SURVEY.md §8d);
+        "step" = both."""
+        p, d, e, m, C = self.p, self.d, self.e, len(self.lost), self.chunk
+        enc = p * (d + e) * C
+        reb = p * (d + m) * C if m else 0
+        return {"encode": enc, "rebuild": reb, "step": enc + reb}[op]
+
+    def exchanged_bytes(self, op: str = "step") -> int:
+        """Bytes this GPU sends over the fabric per operation."""
         if self.world == 1:
             return 0
-        frac = (self.world - 1) / self.world
-        p, d, e, C, m = self.p, self.d, self.e, self.chunk, len(self.lost)
-        enc = (p * d + p * e) * C * frac
-        reb = ((p - m) * (d + e) + m * (d + e)) * C * frac
-        return int(enc + reb)
+        if self._gather_ops is None:
+            self._build_rebuild_gather()
+        if self._return_ops is None:
+            self._build_return()
+        enc = (self.world - 1) * (self.D_host[0].numel() + self.P_host[0].numel())
+        reb = self._gather_sent + self._return_sent
+        return {"encode": enc, "rebuild": reb, "step": enc + reb}[op]
 
     def phase_ms(self) -> dict:
         """Mean milliseconds per phase over the steps marked so far."""
@@ -238,7 +359,7 @@ class ShardedSetRunner:
         acc, n = {}, {}
         ev = self._events
         for (a, ea), (b, eb) in zip(ev, ev[1:]):
-            if a.split("_")[0] != b.split("_")[0]:
+            if a.split("_")[0] != b.split("_")[0] or a.endswith("_done"):
                 continue
             key = f"{a}->{b.split('_', 1)[1]}"
             acc[key] = acc.get(key, 0.0) + ea.elapsed_time(eb)
@@ -248,13 +369,15 @@ class ShardedSetRunner:
     def reset_timing(self) -> None:
         self._events = []
 
-    def report(self, step_seconds: float) -> dict:
+    def report(self, step_seconds: float, op: str = "step") -> dict:
+        coll = {"encode": "RCCL all_to_all (data slices, then parity slices)",
+                "rebuild": "batched RCCL P2P: decode inputs' slices in, rebuilt slices back to their hosts"}
         return {
             "exchange": {
-                "bytes_sent_per_gpu_per_step": self.exchanged_bytes,
+                "bytes_sent_per_gpu_per_step": self.exchanged_bytes(op),
                 "column_slice_bytes": self.W,
-                "collective": "RCCL all_to_all (data / parity slices) + batched P2P (rebuilt slices)",
+                "collective": coll.get(op, coll["encode"] + "; " + coll["rebuild"]),
                 "phase_ms_rank0": self.phase_ms() if self.timing else None,
             },
-            "per_gpu_GBps": round(self.algorithmic_bytes / step_seconds / 1e9, 2),
+            "per_gpu_GBps": round(self.algorithmic_bytes(op) / step_seconds / 1e9, 2),
         }

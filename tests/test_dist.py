@@ -77,11 +77,18 @@ def _worker(rank, world, port, p, e, chunk, lost, outdir):
     np.save(os.path.join(outdir, f"data_{rank}.npy"), runner.D_host.numpy())
     runner.encode()
     np.save(os.path.join(outdir, f"par_{rank}.npy"), runner.P_host.numpy())
+    snap = runner.lost_snapshot()
     runner.erase()
+    assert not snap or not runner.matches(snap)
     # nothing from the encode may survive into the rebuild's gathered slices
     runner.D_gath.fill_(0xA5)
     runner.P_gath.fill_(0x5A)
     runner.rebuild()
+    assert runner.matches(snap)
+    with open(os.path.join(outdir, f"sent_{rank}.json"), "w") as f:
+        import json
+
+        json.dump({"rebuild": runner.exchanged_bytes("rebuild"), "W": runner.W}, f)
     np.save(os.path.join(outdir, f"data2_{rank}.npy"), runner.D_host.numpy())
     np.save(os.path.join(outdir, f"par2_{rank}.npy"), runner.P_host.numpy())
     dist.barrier()
@@ -99,7 +106,7 @@ def _assemble(host_arrays, where, world, p, chunk, W, k, r):
     return np.concatenate(cells)
 
 
-@pytest.mark.parametrize("world,p,e,chunk,lost", [(2, 4, 2, 3000, [1]), (2, 11, 3, 4096, [1, 2]),
+@pytest.mark.parametrize("world,p,e,chunk,lost", [(2, 4, 2, 3000, [1]), (2, 11, 3, 4096, [1, 2]), (4, 11, 3, 2048, [1, 2]),
                                                    (3, 5, 2, 1000, [0, 4])])
 def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost):
     port = _free_port()
@@ -112,6 +119,19 @@ def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost):
 
         with open(os.path.join(td, "where.json")) as f:
             where = json.load(f)
+        # fabric bytes: each decode input's slices go to the other GPUs once,
+        # each rebuilt cell's slices come back from them once
+        from redset_amd.dist import rebuild_inputs
+
+        need_d, need_p = rebuild_inputs(p, e, lost)
+        cells_in = sum(int(need_d[r].sum() + need_p[r].sum()) for r in range(p))
+        want_sent = world * (world - 1) * W * (cells_in + len(lost) * p)
+        sent = 0
+        for g in range(world):
+            with open(os.path.join(td, f"sent_{g}.json")) as f:
+                sent += json.load(f)["rebuild"]
+        assert sent == want_sent
+        assert cells_in == p * (p - e)
         st = oracle.OracleRS(p, e)
         for k in range(world):
             lofi = [_assemble(data, where, world, p, chunk, W, k, r) for r in range(p)]
@@ -122,3 +142,28 @@ def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost):
                 # rebuild restored every member, lost ones included
                 assert np.array_equal(_assemble(data2, where, world, p, chunk, W, k, r), lofi[r]), (k, r)
                 assert np.array_equal(_assemble(par2, where, world, p, chunk, W, k, r), want[r]), (k, r)
+
+
+@pytest.mark.parametrize("p,e,lost", [(11, 3, [1, 2]), (4, 2, [1]), (20, 4, [0, 5, 19]), (6, 3, [2]), (11, 3, [4, 7, 10])])
+def test_rebuild_inputs_read_d_cells_per_stripe(p, e, lost):
+    """The sharded rebuild moves only the cells the decode reads: exactly d
+    surviving cells per stripe (an MDS decode from an information set uses
+    every one of them with a nonzero coefficient), all surviving data among
+    them, never a lost member's."""
+    from redset_amd import codec
+    from redset_amd.dist import rebuild_inputs
+
+    need_d, need_p = rebuild_inputs(p, e, lost)
+    d = p - e
+    rs = codec.RSCodec(p, e)
+    for s in lost:
+        assert not need_d[s].any() and not need_p[s].any()
+    for c in range(p):
+        used = 0
+        for s in range(p):
+            enc = rs.encoding_id(s, c)
+            used += bool(need_d[s, rs.data_id(s, c)]) if enc < p else bool(need_p[s, enc - p])
+        assert used == d, c
+    for s in range(p):
+        if s not in lost:
+            assert need_d[s].all()

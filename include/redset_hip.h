@@ -73,6 +73,8 @@ int redset_hip_rs_create(int ranks, int encoding, redset_hip_rs** out);
 void redset_hip_rs_destroy(redset_hip_rs* rs);
 /* Copies the (p+e) x p matrix (state->mat, src/redset_internal.h:88) as bytes. */
 int redset_hip_rs_matrix(const redset_hip_rs* rs, unsigned char* mat_out);
+/* ranks (p) and encoding (e) of a codec (d->ranks, state->encoding). */
+int redset_hip_rs_shape(const redset_hip_rs* rs, int* ranks, int* encoding);
 /* Same results as redset_rs_get_encoding_id / redset_rs_get_data_id
  * (src/redset_reedsolomon_common.c:822-853). */
 int redset_hip_rs_get_encoding_id(int ranks, int encoding, int rank, int chunk_id);
@@ -117,7 +119,9 @@ void redset_hip_plan_destroy(redset_hip_plan* plan);
 /* ---- stripe primitives (one stripe, device pointers) ----------------- */
 
 /* out[j] = (out[j] ^) sum_i coeffs[j*nin + i] * in[i] over GF(2^8), for
- * nbytes bytes; nin <= 16, nout <= 4 per call. One pass replaces nout*nin
+ * nbytes bytes; 1 <= nin, nout <= 256. Up to 16 inputs x 4 outputs run as
+ * one kernel pass; wider calls run 16-input accumulate passes per group of
+ * 4 outputs (outputs must not alias inputs then). One pass replaces nout*nin
  * calls of redset_rs_reduce_buffer_multadd (src/redset_reedsolomon_common.c:
  * 786-819) and, with a decode matrix, redset_rs_reduce_decode +
  * redset_rs_gaussian_solve (:855-899, :570-630). */
@@ -125,7 +129,7 @@ int redset_hip_gf_combine(const unsigned char* const* in, int nin, unsigned char
                           int nout, const unsigned char* coeffs, size_t nbytes, int accumulate,
                           void* stream);
 
-/* out = (out ^) XOR of nin inputs, nin <= 16 (reduce_xor, src/redset_xor.c:35-42). */
+/* out = (out ^) XOR of nin inputs, 1 <= nin <= 256 (reduce_xor, src/redset_xor.c:35-42). */
 int redset_hip_xor_combine(const unsigned char* const* in, int nin, unsigned char* out,
                            size_t nbytes, int accumulate, void* stream);
 
@@ -215,6 +219,10 @@ void redset_hip_fileio_destroy(redset_hip_fileio* f);
 
 /* Text of the last failure on this thread ("" if none). */
 const char* redset_hip_last_error(void);
+/* For layers built on this library (the per-rank backends of
+ * redset_hip_mpi.h): record `msg` as this thread's last failure; returns
+ * REDSET_FAILURE. */
+int redset_hip_record_error(const char* msg);
 /* Library version string. */
 const char* redset_hip_version(void);
 

@@ -28,6 +28,7 @@ EXPORTED_SYMBOLS = (
     "redset_hip_rs_create",
     "redset_hip_rs_destroy",
     "redset_hip_rs_matrix",
+    "redset_hip_rs_shape",
     "redset_hip_rs_get_encoding_id",
     "redset_hip_rs_get_data_id",
     "redset_hip_rs_plan_encode",
@@ -41,6 +42,7 @@ EXPORTED_SYMBOLS = (
     "redset_hip_xor_combine",
     "redset_hip_rs_decode_matrix",
     "redset_hip_last_error",
+    "redset_hip_record_error",
     "redset_hip_version",
     "redset_hip_rs_encode_stream",
     "redset_hip_rs_rebuild_stream",
@@ -104,6 +106,7 @@ _SIGNATURES = {
     "redset_hip_rs_create": (c_int, [c_int, c_int, POINTER(c_void_p)]),
     "redset_hip_rs_destroy": (None, [c_void_p]),
     "redset_hip_rs_matrix": (c_int, [c_void_p, POINTER(c_ubyte)]),
+    "redset_hip_rs_shape": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
     "redset_hip_rs_get_encoding_id": (c_int, [c_int, c_int, c_int, c_int]),
     "redset_hip_rs_get_data_id": (c_int, [c_int, c_int, c_int, c_int]),
     "redset_hip_rs_plan_encode": (c_int, [c_void_p, _PP, _PP, c_size_t, c_size_t, POINTER(c_void_p)]),
@@ -133,6 +136,7 @@ _SIGNATURES = {
     ),
     "redset_hip_fileio_destroy": (None, [c_void_p]),
     "redset_hip_last_error": (c_char_p, []),
+    "redset_hip_record_error": (c_int, [c_char_p]),
     "redset_hip_version": (c_char_p, []),
 }
 

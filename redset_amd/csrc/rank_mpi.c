@@ -1,0 +1,470 @@
+/*
+ * rank_mpi.c -- per-rank MPI backends (include/redset_hip_mpi.h): the
+ * reference's backend-slot functions, host code in C, with the arithmetic on
+ * the GPU through the codec's C ABI (include/redset_hip.h).
+ *
+ * Each function keeps the reference's slice loop and MPI exchange pattern and
+ * replaces the per-step host multadds with one gf_mac / xor kernel call per
+ * slice over all inputs that slice gathered. Host buffers are page-locked so
+ * the H2D / D2H copies run at PCIe rate; MPI sees host memory (no GPU-aware
+ * MPI needed). The only HIP calls made here are the runtime's C API for
+ * pinned memory, copies and one stream; every kernel is reached through
+ * redset_hip_gf_combine / redset_hip_xor_combine.
+ */
+#define _GNU_SOURCE
+#include "redset_hip_mpi.h"
+
+#include <errno.h>
+#include <hip/hip_runtime_api.h>
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#define DEFAULT_BUF ((size_t) 1 << 20) /* redset_mpi_buf_size default, src/redset.c:45 */
+#define MAX_SCRATCH 8
+
+static int fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+static int fail(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  return redset_hip_record_error(buf); /* REDSET_FAILURE */
+}
+
+static size_t min_sz(size_t a, size_t b) { return a < b ? a : b; }
+
+/* ---- page-locked host + device scratch and one stream, per call -------- */
+
+typedef struct {
+  void* host[MAX_SCRATCH];
+  void* dev[MAX_SCRATCH];
+  int nhost, ndev;
+  hipStream_t stream;
+  int rc;
+} scratch;
+
+static void scratch_init(scratch* S) {
+  memset(S, 0, sizeof(*S));
+  if (hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) != hipSuccess) {
+    S->stream = NULL;
+    S->rc = fail("hipStreamCreate failed");
+  }
+}
+
+static uint8_t* scratch_host(scratch* S, size_t n) {
+  void* p = NULL;
+  if (S->rc || S->nhost == MAX_SCRATCH) return NULL;
+  if (hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault) != hipSuccess) {
+    S->rc = fail("hipHostMalloc(%zu) failed", n);
+    return NULL;
+  }
+  S->host[S->nhost++] = p;
+  return (uint8_t*) p;
+}
+
+static uint8_t* scratch_dev(scratch* S, size_t n) {
+  void* p = NULL;
+  if (S->rc || S->ndev == MAX_SCRATCH) return NULL;
+  if (hipMalloc(&p, n ? n : 1) != hipSuccess) {
+    S->rc = fail("hipMalloc(%zu) failed", n);
+    return NULL;
+  }
+  S->dev[S->ndev++] = p;
+  return (uint8_t*) p;
+}
+
+static void scratch_free(scratch* S) {
+  if (S->stream) (void) hipStreamSynchronize(S->stream);
+  for (int i = 0; i < S->nhost; ++i) (void) hipHostFree(S->host[i]);
+  for (int i = 0; i < S->ndev; ++i) (void) hipFree(S->dev[i]);
+  if (S->stream) (void) hipStreamDestroy(S->stream);
+}
+
+static int h2d(scratch* S, void* dst, const void* src, size_t n) {
+  return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, S->stream) == hipSuccess ? 0 : fail("H2D copy failed");
+}
+
+static int d2h(scratch* S, void* dst, const void* src, size_t n) {
+  return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, S->stream) == hipSuccess ? 0 : fail("D2H copy failed");
+}
+
+static int sync_stream(scratch* S) {
+  return hipStreamSynchronize(S->stream) == hipSuccess ? 0 : fail("hipStreamSynchronize failed");
+}
+
+/* ---- file I/O: full pread / pwrite (redset_read_attempt /
+ * redset_write_attempt, src/redset_io.c:234-310) --------------------------- */
+
+static int pread_full(int fd, void* buf, size_t n, off_t off) {
+  char* p = (char*) buf;
+  while (n) {
+    ssize_t k = pread(fd, p, n, off);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return -1;
+    p += k;
+    n -= (size_t) k;
+    off += k;
+  }
+  return 0;
+}
+
+static int pwrite_full(int fd, const void* buf, size_t n, off_t off) {
+  const char* p = (const char*) buf;
+  while (n) {
+    ssize_t k = pwrite(fd, p, n, off);
+    if (k < 0 && errno == EINTR) continue;
+    if (k <= 0) return -1;
+    p += k;
+    n -= (size_t) k;
+    off += k;
+  }
+  return 0;
+}
+
+static int comm_geometry(MPI_Comm comm, int* ranks, int* rank) {
+  if (MPI_Comm_size(comm, ranks) != MPI_SUCCESS || MPI_Comm_rank(comm, rank) != MPI_SUCCESS)
+    return fail("MPI_Comm_size/rank failed");
+  return 0;
+}
+
+/* header size = where the caller left fd_chunk (src/redset_reedsolomon.c:295, :588) */
+static int header_size(int fd_chunk, const char* chunk_file, off_t* header) {
+  *header = lseek(fd_chunk, 0, SEEK_CUR);
+  if (*header < 0) return fail("lseek(%s) failed", chunk_file ? chunk_file : "chunk file");
+  return 0;
+}
+
+/* member t's logical-file segment in XOR stripe c (src/redset_xor.c:251-266) */
+static int xor_segment(int t, int c) { return c < t ? c : c - 1; }
+
+/* ---- RS encode (replaces redset_reedsolomon_encode, src/redset_reedsolomon.c:280-402) */
+
+int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi,
+                              const char* chunk_file, int fd_chunk, size_t chunk_size, size_t buf_size) {
+  int p, r, rp, e;
+  off_t header;
+  if (!rs || !lofi || !lofi->read) return fail("rs_encode_rank: null argument");
+  if (comm_geometry(comm, &p, &r) || redset_hip_rs_shape(rs, &rp, &e)) return REDSET_FAILURE;
+  if (p != rp) return fail("communicator has %d ranks, codec %d", p, rp);
+  if (header_size(fd_chunk, chunk_file, &header)) return REDSET_FAILURE;
+  const int d = p - e;
+  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+
+  unsigned char* mat = malloc((size_t) (p + e) * p);
+  unsigned char* coef = malloc((size_t) e * d);       /* [slot i][ring step s] */
+  const unsigned char** ins = malloc(sizeof(*ins) * (size_t) d);
+  MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) e);
+  scratch S;
+  scratch_init(&S);
+  uint8_t* h_send = scratch_host(&S, B);
+  uint8_t* h_recv = scratch_host(&S, (size_t) d * e * B); /* [step s][slot i] */
+  uint8_t* h_par = scratch_host(&S, (size_t) e * B);
+  uint8_t* d_recv = scratch_dev(&S, (size_t) d * e * B);
+  uint8_t* d_par = scratch_dev(&S, (size_t) e * B);
+  int rc = S.rc;
+  if (!rc && (!mat || !coef || !ins || !req)) rc = fail("out of host memory");
+  if (!rc) rc = redset_hip_rs_matrix(rs, mat);
+  if (rc) goto out;
+
+  /* slot i's coefficients over the d slices it receives, in ring-step order:
+   * at step s (chunk_step p-1-s) slot i receives from r + (p - chunk_step + i) */
+  for (int i = 0; i < e; ++i)
+    for (int s = 0; s < d; ++s) {
+      const int step = p - 1 - s;
+      const int sender = (r + (p - step + i)) % p;
+      coef[(size_t) i * d + s] = mat[(size_t) (p + i) * p + sender];
+    }
+
+  for (size_t nread = 0; nread < chunk_size; nread += B) {
+    const size_t count = min_sz(B, chunk_size - nread);
+    for (int s = 0; s < d; ++s) { /* chunk_step = p-1 .. e, src/redset_reedsolomon.c:329-377 */
+      const int step = p - 1 - s;
+      const int chunk_id = (r + step) % p;
+      const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
+      if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0) rc = fail("lofi read failed");
+      int k = 0;
+      for (int i = 0; i < e; ++i) {
+        const int dist = p - step + i;
+        MPI_Irecv(h_recv + ((size_t) s * e + i) * B, (int) count, MPI_BYTE, (r + dist) % p, 0, comm, &req[k++]);
+        MPI_Isend(h_send, (int) count, MPI_BYTE, (r - dist + p) % p, 0, comm, &req[k++]);
+      }
+      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+    }
+    /* all d*e slices of this window: one H2D, one kernel per slot, one D2H */
+    int grc = h2d(&S, d_recv, h_recv, (size_t) d * e * B);
+    for (int i = 0; i < e && !grc; ++i) {
+      for (int s = 0; s < d; ++s) ins[s] = d_recv + ((size_t) s * e + i) * B;
+      unsigned char* o = d_par + (size_t) i * B;
+      grc = redset_hip_gf_combine(ins, d, &o, 1, coef + (size_t) i * d, count, 0, S.stream);
+    }
+    if (!grc) grc = d2h(&S, h_par, d_par, (size_t) e * B);
+    if (!grc) grc = sync_stream(&S);
+    if (grc) { /* a device failure is not recoverable mid-collective */
+      rc = grc;
+      goto out;
+    }
+    for (int i = 0; i < e; ++i) { /* :379-388 */
+      const off_t off = header + (off_t) i * (off_t) chunk_size + (off_t) nread;
+      if (pwrite_full(fd_chunk, h_par + (size_t) i * B, count, off) != 0) rc = fail("write %s failed", chunk_file);
+    }
+  }
+out:
+  scratch_free(&S);
+  free(mat);
+  free(coef);
+  free(ins);
+  free(req);
+  return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+/* ---- RS decode (replaces redset_reedsolomon_decode, src/redset_reedsolomon.c:570-785) */
+
+int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missing, const int* rebuild_ranks,
+                              int need_rebuild, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
+                              size_t chunk_size, size_t buf_size) {
+  int p, r, rp, e;
+  off_t header;
+  if (!rs || !lofi || !rebuild_ranks) return fail("rs_decode_rank: null argument");
+  if (comm_geometry(comm, &p, &r) || redset_hip_rs_shape(rs, &rp, &e)) return REDSET_FAILURE;
+  if (p != rp) return fail("communicator has %d ranks, codec %d", p, rp);
+  if (missing < 1 || missing > e) return fail("cannot rebuild %d members with %d encoding blocks", missing, e);
+  if (header_size(fd_chunk, chunk_file, &header)) return REDSET_FAILURE;
+  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+
+  unsigned char* D = malloc((size_t) missing * p); /* decode map of stripe r: missing x p */
+  unsigned char* coef = malloc((size_t) missing * p);
+  int* cols = malloc(sizeof(int) * (size_t) p);
+  const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
+  unsigned char** outs = malloc(sizeof(*outs) * (size_t) missing);
+  MPI_Request* req = malloc(sizeof(*req) * (size_t) (2 * p + missing + 2));
+  scratch S;
+  scratch_init(&S);
+  uint8_t* h_send = scratch_host(&S, B);
+  uint8_t* h_cells = scratch_host(&S, (size_t) p * B);  /* member s's cell of stripe r */
+  uint8_t* h_out = scratch_host(&S, (size_t) missing * B);
+  uint8_t* h_gather = scratch_host(&S, (size_t) p * B); /* rebuilt cells from every solver */
+  uint8_t* d_cells = scratch_dev(&S, (size_t) p * B);
+  uint8_t* d_out = scratch_dev(&S, (size_t) missing * B);
+  int rc = S.rc;
+  if (!rc && (!D || !coef || !cols || !ins || !outs || !req)) rc = fail("out of host memory");
+  /* member r solves stripe r (decode_chunk_id = rank, :607-611): one linear
+   * map equal to redset_rs_reduce_decode + redset_rs_gaussian_solve */
+  if (!rc) rc = redset_hip_rs_decode_matrix(rs, missing, rebuild_ranks, r, D);
+  if (rc) goto out;
+  int ncols = 0;
+  for (int s = 0; s < p; ++s) {
+    int used = 0;
+    for (int i = 0; i < missing; ++i) used |= D[(size_t) i * p + s] != 0;
+    if (used) cols[ncols++] = s;
+  }
+  for (int i = 0; i < missing; ++i)
+    for (int k = 0; k < ncols; ++k) coef[(size_t) i * ncols + k] = D[(size_t) i * p + cols[k]];
+  for (int k = 0; k < ncols; ++k) ins[k] = d_cells + (size_t) cols[k] * B;
+  for (int i = 0; i < missing; ++i) outs[i] = d_out + (size_t) i * B;
+
+  for (size_t nread = 0; nread < chunk_size; nread += B) {
+    const size_t count = min_sz(B, chunk_size - nread);
+    for (int step = 0; step < p; ++step) { /* :646-703 */
+      const int lhs = (r - step + p) % p, rhs = (r + step) % p;
+      const int chunk_id = (r + step) % p;
+      const int enc = redset_hip_rs_get_encoding_id(p, e, r, chunk_id);
+      if (!need_rebuild) {
+        if (enc < p) {
+          const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
+          if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0)
+            rc = fail("lofi read failed");
+        } else {
+          const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) nread;
+          if (pread_full(fd_chunk, h_send, count, off) != 0) rc = fail("read %s failed", chunk_file);
+        }
+      } else {
+        memset(h_send, 0, count); /* an erased member contributes nothing */
+      }
+      if (step > 0) {
+        MPI_Irecv(h_cells + (size_t) lhs * B, (int) count, MPI_BYTE, lhs, 0, comm, &req[0]);
+        MPI_Isend(h_send, (int) count, MPI_BYTE, rhs, 0, comm, &req[1]);
+        MPI_Waitall(2, req, MPI_STATUSES_IGNORE);
+      } else {
+        memcpy(h_cells + (size_t) r * B, h_send, count);
+      }
+    }
+    int grc = h2d(&S, d_cells, h_cells, (size_t) p * B);
+    if (!grc && ncols > 0) grc = redset_hip_gf_combine(ins, ncols, outs, missing, coef, count, 0, S.stream);
+    if (!grc) grc = d2h(&S, h_out, d_out, (size_t) missing * B);
+    if (!grc) grc = sync_stream(&S);
+    if (grc) {
+      rc = grc;
+      goto out;
+    }
+    /* gather rebuilt cells to the erased members, :713-733 */
+    int k = 0;
+    if (need_rebuild)
+      for (int step = 0; step < p; ++step) {
+        const int lhs = (r - step + p) % p;
+        MPI_Irecv(h_gather + (size_t) lhs * B, (int) count, MPI_BYTE, lhs, 0, comm, &req[k++]);
+      }
+    for (int i = 0; i < missing; ++i)
+      MPI_Isend(h_out + (size_t) i * B, (int) count, MPI_BYTE, rebuild_ranks[i], 0, comm, &req[k++]);
+    MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+    if (need_rebuild) { /* :736-765 */
+      for (int step = 0; step < p; ++step) {
+        const int lhs = (r - step + p) % p;
+        const int enc = redset_hip_rs_get_encoding_id(p, e, r, lhs);
+        const uint8_t* cell = h_gather + (size_t) lhs * B;
+        if (enc < p) {
+          const int seg = redset_hip_rs_get_data_id(p, e, r, lhs);
+          if (!lofi->write || lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, cell) != 0)
+            rc = fail("lofi write failed");
+        } else {
+          const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) nread;
+          if (pwrite_full(fd_chunk, cell, count, off) != 0) rc = fail("write %s failed", chunk_file);
+        }
+      }
+    }
+  }
+out:
+  scratch_free(&S);
+  free(D);
+  free(coef);
+  free(cols);
+  free(ins);
+  free(outs);
+  free(req);
+  return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+/* ---- XOR encode (replaces redset_xor_encode, src/redset_xor.c:220-295) */
+
+int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
+                               size_t chunk_size, size_t buf_size) {
+  int p, r;
+  off_t header;
+  if (!lofi || !lofi->read) return fail("xor_encode_rank: null argument");
+  if (comm_geometry(comm, &p, &r)) return REDSET_FAILURE;
+  if (p < 2) return fail("XOR needs at least 2 ranks");
+  if (header_size(fd_chunk, chunk_file, &header)) return REDSET_FAILURE;
+  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+
+  const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
+  MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) p);
+  scratch S;
+  scratch_init(&S);
+  uint8_t* h_send = scratch_host(&S, (size_t) p * B); /* my cell of stripe t, for t != r */
+  uint8_t* h_recv = scratch_host(&S, (size_t) p * B); /* member t's cell of stripe r */
+  uint8_t* h_out = scratch_host(&S, B);
+  uint8_t* d_recv = scratch_dev(&S, (size_t) p * B);
+  uint8_t* d_out = scratch_dev(&S, B);
+  int rc = S.rc;
+  if (!rc && (!ins || !req)) rc = fail("out of host memory");
+  if (rc) goto out;
+  int nin = 0;
+  for (int t = 0; t < p; ++t)
+    if (t != r) ins[nin++] = d_recv + (size_t) t * B;
+
+  for (size_t nread = 0; nread < chunk_size; nread += B) {
+    const size_t count = min_sz(B, chunk_size - nread);
+    int k = 0;
+    /* the ring of src/redset_xor.c:251-285 leaves member r with the XOR of
+     * every other member's cell of stripe r; exchange those cells directly */
+    for (int t = 0; t < p; ++t) {
+      if (t == r) continue;
+      if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, t), nread, count, h_send + (size_t) t * B) != 0)
+        rc = fail("lofi read failed");
+      MPI_Irecv(h_recv + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
+      MPI_Isend(h_send + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
+    }
+    MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+    int grc = h2d(&S, d_recv, h_recv, (size_t) p * B);
+    if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out, count, 0, S.stream);
+    if (!grc) grc = d2h(&S, h_out, d_out, count);
+    if (!grc) grc = sync_stream(&S);
+    if (grc) {
+      rc = grc;
+      goto out;
+    }
+    if (pwrite_full(fd_chunk, h_out, count, header + (off_t) nread) != 0) /* :280-284 */
+      rc = fail("write %s failed", chunk_file);
+  }
+out:
+  scratch_free(&S);
+  free(ins);
+  free(req);
+  return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+/* ---- XOR decode (replaces redset_xor_decode, src/redset_xor.c:441-531) */
+
+int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
+                               int fd_chunk, size_t chunk_size, size_t buf_size) {
+  int p, r;
+  off_t header;
+  if (!lofi || !lofi->read) return fail("xor_decode_rank: null argument");
+  if (comm_geometry(comm, &p, &r)) return REDSET_FAILURE;
+  if (root < 0 || root >= p) return fail("root %d out of range", root);
+  if (header_size(fd_chunk, chunk_file, &header)) return REDSET_FAILURE;
+  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+
+  const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
+  MPI_Request* req = malloc(sizeof(*req) * (size_t) p);
+  scratch S;
+  scratch_init(&S);
+  uint8_t* h_cells = scratch_host(&S, (size_t) p * B);
+  uint8_t* h_out = scratch_host(&S, B);
+  uint8_t* d_cells = scratch_dev(&S, (size_t) p * B);
+  uint8_t* d_out = scratch_dev(&S, B);
+  int rc = S.rc;
+  if (!rc && (!ins || !req)) rc = fail("out of host memory");
+  if (rc) goto out;
+  int nin = 0;
+  for (int t = 0; t < p; ++t)
+    if (t != root) ins[nin++] = d_cells + (size_t) t * B;
+
+  /* stripe by stripe, as the reference's pipelined reduce to the root
+   * (src/redset_xor.c:466-524): every survivor sends its cell of stripe c,
+   * the root XORs them on the GPU and writes its own cell of stripe c */
+  for (int c = 0; c < p; ++c) {
+    for (size_t nread = 0; nread < chunk_size; nread += B) {
+      const size_t count = min_sz(B, chunk_size - nread);
+      if (r != root) {
+        uint8_t* mine = h_cells + (size_t) r * B;
+        if (c != r) {
+          if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, c), nread, count, mine) != 0)
+            rc = fail("lofi read failed");
+        } else if (pread_full(fd_chunk, mine, count, header + (off_t) nread) != 0) {
+          rc = fail("read %s failed", chunk_file);
+        }
+        MPI_Send(mine, (int) count, MPI_BYTE, root, 0, comm);
+        continue;
+      }
+      int k = 0;
+      for (int t = 0; t < p; ++t)
+        if (t != root) MPI_Irecv(h_cells + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
+      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+      int grc = h2d(&S, d_cells, h_cells, (size_t) p * B);
+      if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out, count, 0, S.stream);
+      if (!grc) grc = d2h(&S, h_out, d_out, count);
+      if (!grc) grc = sync_stream(&S);
+      if (grc) {
+        rc = grc;
+        goto out;
+      }
+      if (c != root) {
+        if (!lofi->write ||
+            lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(root, c), nread, count, h_out) != 0)
+          rc = fail("lofi write failed");
+      } else if (pwrite_full(fd_chunk, h_out, count, header + (off_t) nread) != 0) {
+        rc = fail("write %s failed", chunk_file);
+      }
+    }
+  }
+out:
+  scratch_free(&S);
+  free(ins);
+  free(req);
+  return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}

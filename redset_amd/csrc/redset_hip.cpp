@@ -33,6 +33,9 @@ using redset_hip::StripeMap;
 using redset_hip::XorJob;
 using redset_hip::XorLaunch;
 
+// widest stripe primitive call: p + e <= 256 bounds any redset stripe
+constexpr int kMaxCombine = 256;
+
 struct redset_hip_plan {
   redset_hip_plan_info info{};
   GfJob* d_gf = nullptr;  // device job arrays
@@ -237,7 +240,7 @@ int finish_plan(int kind, int ranks, int encoding, int missing, size_t chunk, co
 namespace redset_hip {
 
 int run_stripe(const StripeMap& m, const uint8_t* const* in, uint8_t* const* out, size_t nbytes, void* stream,
-               int blocks_total) {
+               int blocks_total, bool accumulate) {
   const int nin = static_cast<int>(m.in.size()), nt = static_cast<int>(m.out.size());
   for (int og = 0; og * kMaxOut < nt; ++og) {
     const int o0 = og * kMaxOut, no = std::min(kMaxOut, nt - o0);
@@ -258,7 +261,7 @@ int run_stripe(const StripeMap& m, const uint8_t* const* in, uint8_t* const* out
         std::memset(&X, 0, sizeof(X));
         X.njobs = 1;
         X.nin = ni;
-        X.accumulate = ig > 0;
+        X.accumulate = accumulate || ig > 0;
         X.bytes_only = al ? 0 : 1;
         X.nbytes = nbytes;
         X.blocks_per_job = blocks_per_job(1, nbytes, 8, blocks_total);
@@ -280,7 +283,7 @@ int run_stripe(const StripeMap& m, const uint8_t* const* in, uint8_t* const* out
         G.njobs = 1;
         G.nin = ni;
         G.nout = no;
-        G.accumulate = ig > 0;
+        G.accumulate = accumulate || ig > 0;
         G.bytes_only = al ? 0 : 1;
         G.nbytes = nbytes;
         G.blocks_per_job = blocks_per_job(1, nbytes, gf_blocks_per_cu(ni), blocks_total);
@@ -297,6 +300,14 @@ int run_stripe(const StripeMap& m, const uint8_t* const* in, uint8_t* const* out
 extern "C" {
 
 const char* redset_hip_last_error(void) { return redset_hip::last_error(); }
+int redset_hip_record_error(const char* msg) { return fail("%s", msg ? msg : "unknown error"); }
+
+int redset_hip_rs_shape(const redset_hip_rs* rs, int* ranks, int* encoding) {
+  if (!rs) return fail("rs_shape: null codec");
+  if (ranks) *ranks = rs->ranks;
+  if (encoding) *encoding = rs->encoding;
+  return REDSET_SUCCESS;
+}
 const char* redset_hip_version(void) { return "redset-hip 0.2 (gfx950)"; }
 
 int redset_hip_rs_create(int ranks, int encoding, redset_hip_rs** out) {
@@ -419,9 +430,21 @@ void redset_hip_plan_destroy(redset_hip_plan* plan) {
 
 int redset_hip_gf_combine(const unsigned char* const* in, int nin, unsigned char* const* out, int nout,
                           const unsigned char* coeffs, size_t nbytes, int accumulate, void* stream) {
-  if (nin < 1 || nin > kMaxIn || nout < 1 || nout > kMaxOut)
-    return fail("gf_combine: nin=%d (1..%d), nout=%d (1..%d)", nin, kMaxIn, nout, kMaxOut);
+  if (nin < 1 || nin > kMaxCombine || nout < 1 || nout > kMaxCombine)
+    return fail("gf_combine: nin=%d, nout=%d (1..%d)", nin, nout, kMaxCombine);
   if (!in || !out || !coeffs) return fail("gf_combine: null argument");
+  if (nin > kMaxIn || nout > kMaxOut) {
+    // wider than one kernel pass: 16-input accumulate passes x 4-output groups
+    redset_hip::StripeMap m;
+    m.in.resize(nin);
+    m.out.resize(nout);
+    m.coef.assign(coeffs, coeffs + static_cast<size_t>(nin) * nout);
+    for (int i = 0; i < nin; ++i)
+      if (!in[i]) return fail("gf_combine: null input %d", i);
+    for (int j = 0; j < nout; ++j)
+      if (!out[j]) return fail("gf_combine: null output %d", j);
+    return redset_hip::run_stripe(m, in, out, nbytes, stream, 0, accumulate != 0);
+  }
   GfJob J;
   std::memset(&J, 0, sizeof(J));
   bool al = true;
@@ -450,8 +473,18 @@ int redset_hip_gf_combine(const unsigned char* const* in, int nin, unsigned char
 
 int redset_hip_xor_combine(const unsigned char* const* in, int nin, unsigned char* out, size_t nbytes, int accumulate,
                            void* stream) {
-  if (nin < 1 || nin > kMaxIn) return fail("xor_combine: nin=%d (1..%d)", nin, kMaxIn);
+  if (nin < 1 || nin > kMaxCombine) return fail("xor_combine: nin=%d (1..%d)", nin, kMaxCombine);
   if (!in || !out) return fail("xor_combine: null argument");
+  if (nin > kMaxIn) {
+    redset_hip::StripeMap m;
+    m.in.resize(nin);
+    m.out.resize(1);
+    m.coef.assign(static_cast<size_t>(nin), 1);
+    m.xor_only = true;
+    for (int i = 0; i < nin; ++i)
+      if (!in[i]) return fail("xor_combine: null input %d", i);
+    return redset_hip::run_stripe(m, in, &out, nbytes, stream, 0, accumulate != 0);
+  }
   XorJob J;
   std::memset(&J, 0, sizeof(J));
   bool al = aligned16(out);

@@ -60,7 +60,8 @@ const char* last_error();
 // Enqueue one stripe's map on `stream` over cells at the given device
 // pointers (in[i] for m.in[i], out[j] for m.out[j]), split into passes of
 // <= 16 inputs x <= 4 outputs. blocks_total: grid size budget (0 = fill GPU).
+// accumulate: XOR into the outputs instead of overwriting them.
 int run_stripe(const StripeMap& m, const uint8_t* const* in, uint8_t* const* out, size_t nbytes, void* stream,
-               int blocks_total);
+               int blocks_total, bool accumulate = false);
 
 }  // namespace redset_hip

@@ -148,3 +148,18 @@ def test_decode_maps_reproduce_oracle_rebuild(hiplib, oracle, p, e):
             got = _apply(D, cells)
             for i, r in enumerate(sorted(lost)):
                 assert np.array_equal(got[i], cell(want_l, want_p, r, c)), (lost, c, r)
+
+
+def test_shape_and_error_recording(hiplib):
+    from ctypes import byref, c_int, c_void_p
+
+    from redset_amd import _lib
+
+    L = _lib.load()
+    h = c_void_p()
+    assert L.redset_hip_rs_create(20, 4, byref(h)) == 0
+    p, e = c_int(), c_int()
+    assert L.redset_hip_rs_shape(h, byref(p), byref(e)) == 0 and (p.value, e.value) == (20, 4)
+    L.redset_hip_rs_destroy(h)
+    assert L.redset_hip_record_error(b"per-rank backend: lofi read failed") == 1
+    assert L.redset_hip_last_error() == b"per-rank backend: lofi read failed"

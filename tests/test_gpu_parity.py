@@ -58,7 +58,8 @@ def gpu_bytes(arr: np.ndarray, offset=0):
 # stripe primitives
 # --------------------------------------------------------------------------
 
-@pytest.mark.parametrize("nin,nout", [(1, 1), (2, 3), (8, 3), (8, 4), (16, 4), (13, 2), (5, 1)])
+@pytest.mark.parametrize("nin,nout", [(1, 1), (2, 3), (8, 3), (8, 4), (16, 4), (13, 2), (5, 1),
+                                      (17, 1), (40, 6), (3, 9), (100, 5)])  # wider: split passes
 @pytest.mark.parametrize("nbytes", [1, 15, 16, 17, 4096 + 7, (1 << 20) + 3])
 def test_gf_combine_matches_numpy(rd, nin, nout, nbytes):
     rng = np.random.default_rng(nin * 100 + nout + nbytes)
@@ -102,7 +103,7 @@ def test_gf_combine_unaligned(rd, offset):
         assert np.array_equal(outs[j][1].cpu().numpy(), want[j])
 
 
-@pytest.mark.parametrize("nin", [1, 2, 7, 16])
+@pytest.mark.parametrize("nin", [1, 2, 7, 16, 33])
 @pytest.mark.parametrize("nbytes,offset", [(33, 0), (1 << 20, 0), (5592406, 0), (4099, 5)])
 def test_xor_combine(rd, nin, nbytes, offset):
     rng = np.random.default_rng(nin + nbytes)
@@ -113,6 +114,9 @@ def test_xor_combine(rd, nin, nbytes, offset):
     rd.xor_combine(d_in, out[1], nbytes)
     torch.cuda.synchronize()
     assert np.array_equal(out[1].cpu().numpy(), want)
+    rd.xor_combine(d_in, out[1], nbytes, accumulate=True)
+    torch.cuda.synchronize()
+    assert not out[1].any().item()
 
 
 # --------------------------------------------------------------------------
@@ -128,6 +132,7 @@ RS_CASES = [
     (12, 6, 8192),        # e > 4: two output groups
     (24, 4, 8192),        # d = 20 > 16: accumulate pass
     (2, 1, 1000),
+    (16, 4, 1),           # smallest chunk redset makes (src/redset_reedsolomon.c:491-493)
 ]
 
 
@@ -192,6 +197,27 @@ def test_rs_rebuild_sampled_patterns(rd, oracle, p, e, chunk, n):
     pats = [(1, 2)] + [tuple(sorted(rng.choice(p, size=int(rng.integers(1, e + 1)), replace=False).tolist()))
                        for _ in range(n)]
     _rebuild_case(rd, oracle, p, e, chunk, pats)
+
+
+@pytest.mark.parametrize("p,e,chunk,lost", [(200, 56, 272, (0, 7, 55, 56, 100, 199)),
+                                             (252, 4, 1027, (3, 4, 5, 251)),
+                                             (128, 127, 48, tuple(range(1, 128)))])
+def test_rs_largest_fields(rd, oracle, p, e, chunk, lost):
+    """p + e up to 256, the GF(2^8) limit (src/redset_reedsolomon.c:174-185):
+    d up to 248 inputs (16-input accumulate passes) and e up to 127 outputs
+    (4-output groups); rebuild with as many erasures as some patterns allow."""
+    if p + e > 256:
+        pytest.skip("beyond the field")
+    lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=p + e)
+    lay = upload_set(rd, lofi, parity, p - e, e, chunk)
+    codec = rd.RSCodec(p, e)
+    codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride).execute()
+    torch.cuda.synchronize()
+    oracle.OracleRS(p, e).encode_set(lofi, parity, chunk)
+    _, got = download_set(lay)
+    for r in range(p):
+        assert np.array_equal(got[r], parity[r]), r
+    _rebuild_case(rd, oracle, p, e, chunk, [tuple(lost[: min(len(lost), e)])])
 
 
 def test_rs_rebuild_unpadded_odd_chunk(rd, oracle):

@@ -41,6 +41,18 @@
 #ifndef REDSET_MEMONLY
 #define REDSET_MEMONLY 0
 #endif
+// Cache policy of the cell streams. Every cell byte is read or written
+// exactly once, so both directions are marked non-temporal (`nt`): +3% on
+// the RS step and +7% on XOR against the default policy, while either one
+// alone gains nothing (nt loads alone lose 2%) -- profiles/r01_ab_cache_policy.txt.
+// A/B knobs (tools/build_ab_variant.sh): stores 0 = default, 1 = nt,
+// 2 = sc0 sc1 nt, 3 = sc1 nt, 4 = sc0 nt, 5 = sc0 sc1; loads 0 = default, 1 = nt.
+#ifndef REDSET_STORE_POLICY
+#define REDSET_STORE_POLICY 1
+#endif
+#ifndef REDSET_LOAD_POLICY
+#define REDSET_LOAD_POLICY 1
+#endif
 
 namespace redset_hip {
 
@@ -125,7 +137,30 @@ typedef __attribute__((address_space(1))) v4u g_u4;
 template <int NIN>
 __device__ __forceinline__ void load_vec(v4u (&x)[NIN], g_cu4* const (&in)[NIN], size_t v) {
 #pragma unroll
-  for (int i = 0; i < NIN; ++i) x[i] = in[i][v];
+  for (int i = 0; i < NIN; ++i) {
+#if REDSET_LOAD_POLICY == 1
+    x[i] = __builtin_nontemporal_load(in[i] + v);
+#else
+    x[i] = in[i][v];
+#endif
+  }
+}
+
+// one 16-B store of an output stream
+__device__ __forceinline__ void store_vec(g_u4* p, size_t v, v4u r) {
+#if REDSET_STORE_POLICY == 1
+  __builtin_nontemporal_store(r, p + v);
+#elif REDSET_STORE_POLICY == 2
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p + v), "v"(r) : "memory");
+#elif REDSET_STORE_POLICY == 3
+  asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p + v), "v"(r) : "memory");
+#elif REDSET_STORE_POLICY == 4
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 nt" ::"v"(p + v), "v"(r) : "memory");
+#elif REDSET_STORE_POLICY == 5
+  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p + v), "v"(r) : "memory");
+#else
+  p[v] = r;
+#endif
 }
 
 // out[j][v] (^)= sum_i coef[j][i] * x[i] for one 16-B position of every cell
@@ -178,7 +213,7 @@ __device__ __forceinline__ void gf_mac_vec(const uint32_t* lds, const v4u (&x)[N
     if constexpr (ACC) {
       if (store) out[j][v] = r ^ out[j][v];
     } else {
-      out[j][v] = r;
+      store_vec(out[j], v, r);
     }
   }
 }
@@ -191,7 +226,7 @@ __device__ __forceinline__ void xor_vec(const v4u (&x)[NIN], g_u4* out, size_t v
   if constexpr (ACC) {
     if (store) out[v] = r ^ out[v];
   } else {
-    out[v] = r;
+    store_vec(out, v, r);
   }
 }
 

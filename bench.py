@@ -229,8 +229,9 @@ def xor_leg(args, chunk, stream):
         "frac": round((eb + rb) / ((t_enc + t_reb) * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
         "encode_GBps": round(eb / (t_enc * 1e-3) / 1e9, 1),
         "rebuild_GBps": round(rb / (t_reb * 1e-3) / 1e9, 1),
-        "avg_launch_ms": {"encode": round(t_enc, 4), "rebuild": round(t_reb, 4)},
-        "algorithmic_bytes_per_launch": {"encode": eb, "rebuild": rb},
+        "launches_per_step": {"encode": enc.launches, "rebuild": reb.launches},
+        "avg_launch_ms": {"encode": round(t_enc / enc.launches, 4), "rebuild": round(t_reb / reb.launches, 4)},
+        "algorithmic_bytes_per_launch": {"encode": eb // enc.launches, "rebuild": rb // reb.launches},
         "round_trip_bit_exact": ok,
     }
 
@@ -364,18 +365,22 @@ def main():
     }
     enc_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
     reb_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
+    # one launch = one stripe when a plan runs its jobs one after another (the
+    # default for 64 MiB cells), else the whole set; a launch's average
+    # duration is the plan's event span / its launches (gaps included)
+    el, rl = enc_plan.launches, reb_plan.launches
+    eb1, rb1 = eb // el, rb // rl
     achieved = (eb + rb) / ((enc_ms + reb_ms) * 1e-3) / 1e9
-    # PMC-measured HBM bytes per gf_mac launch, averaged over the step's
-    # encode and rebuild launches (tools/pmc_traffic.py; gfx950 FETCH_SIZE
-    # doubled); compare with the algorithmic average below
+    # PMC-measured HBM bytes per gf_mac launch (tools/pmc_traffic.py; gfx950
+    # FETCH_SIZE doubled); compare with the algorithmic bytes per launch
     k_enc = f"gf_mac_kernel<{d}, {min(e, 4)}, false>"
     k_reb = f"gf_mac_kernel<{d}, {min(len(lost), 4)}, false>"
     t_enc, t_reb = load_traffic(args.traffic_json, k_enc), load_traffic(args.traffic_json, k_reb)
     # the PMC file is recorded on the default workload; a different set shape
     # or chunk size has different bytes per launch, so it does not apply
-    if not (t_enc and t_reb and 0.5 < t_enc / eb < 2.0 and 0.5 < t_reb / rb < 2.0):
+    if not (t_enc and t_reb and 0.5 < t_enc / eb1 < 2.0 and 0.5 < t_reb / rb1 < 2.0):
         t_enc = t_reb = None
-    traffic = (t_enc + t_reb) // 2 if (t_enc and t_reb) else None
+    traffic = (t_enc * el + t_reb * rl) // (el + rl) if (t_enc and t_reb) else None
     result["roofline"] = {
         "bound": "hbm",
         "kernel": f"{k_enc} (encode) + {k_reb} (rebuild), redset_amd/csrc/codec_device.h",
@@ -384,10 +389,11 @@ def main():
         "unit": "GB/s",
         "frac": round(achieved / HBM_PEAK_GBPS, 4),
         "traffic": traffic,
-        "algorithmic_bytes_per_launch": {"encode": eb, "rebuild": rb, "mean": (eb + rb) // 2},
+        "launches_per_step": {"encode": el, "rebuild": rl},
+        "algorithmic_bytes_per_launch": {"encode": eb1, "rebuild": rb1, "mean": (eb + rb) // (el + rl)},
         "traffic_per_launch": {"encode": t_enc, "rebuild": t_reb},
         "traffic_source": "profiles/traffic_latest.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
-        "avg_launch_ms": {"encode": round(enc_ms, 4), "rebuild": round(reb_ms, 4)},
+        "avg_launch_ms": {"encode": round(enc_ms / el, 4), "rebuild": round(reb_ms / rl, 4)},
     }
     result["breakdown"] = {
         "encode_GBps": round(eb / (enc_ms * 1e-3) / 1e9, 1),

@@ -61,6 +61,12 @@ class Plan:
     def bytes_written(self) -> int:
         return int(self.info.bytes_written)
 
+    @property
+    def launches(self) -> int:
+        """Kernel launches one execute() issues (one per stripe when the
+        plan runs its jobs one after another)."""
+        return int(self.info.launches)
+
     def close(self) -> None:
         if self._h:
             _lib.load().redset_hip_plan_destroy(self._h)

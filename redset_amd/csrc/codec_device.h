@@ -360,8 +360,17 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
 // value in the kernel arguments (stripe primitives, no device descriptor)
 template <int NIN, int NOUT, bool ACC>
 __global__ void __launch_bounds__(kBlock) gf_mac_kernel(GfLaunch L) {
+  if (L.sequential == kJobsInKernel) {
+    // every block sweeps every job in turn: one stripe's cells in flight at
+    // a time, with no launch boundary between stripes
+    for (int j = 0; j < L.njobs; ++j) {
+      if (j > 0) __syncthreads();  // all waves are done with the last job's tables
+      gf_mac_body<NIN, NOUT, ACC>(L, L.jobs[j], blockIdx.x);
+    }
+    return;
+  }
   const int job = blockIdx.x / L.blocks_per_job;
-  gf_mac_body<NIN, NOUT, ACC>(L, L.jobs[job], blockIdx.x - job * L.blocks_per_job);
+  gf_mac_body<NIN, NOUT, ACC>(L, L.jobs[L.job0 + job], blockIdx.x - job * L.blocks_per_job);
 }
 
 template <int NIN, int NOUT, bool ACC>
@@ -371,8 +380,12 @@ __global__ void __launch_bounds__(kBlock) gf_mac_kernel_arg(GfLaunch L, GfJob J)
 
 template <int NIN, bool ACC>
 __global__ void __launch_bounds__(kBlock) xor_kernel(XorLaunch L) {
+  if (L.sequential == kJobsInKernel) {
+    for (int j = 0; j < L.njobs; ++j) xor_body<NIN, ACC>(L, L.jobs[j], blockIdx.x);
+    return;
+  }
   const int job = blockIdx.x / L.blocks_per_job;
-  xor_body<NIN, ACC>(L, L.jobs[job], blockIdx.x - job * L.blocks_per_job);
+  xor_body<NIN, ACC>(L, L.jobs[L.job0 + job], blockIdx.x - job * L.blocks_per_job);
 }
 
 template <int NIN, bool ACC>

@@ -14,6 +14,14 @@ namespace redset_hip {
 constexpr int kMaxIn = 16;
 constexpr int kMaxOut = 4;
 
+// Job order of a launch (GfLaunch / XorLaunch::sequential). 0: all jobs side
+// by side in one grid, blocks_per_job blocks each. kJobsInLaunches: one
+// launch per job over the whole grid. kJobsInKernel: one launch whose every
+// block sweeps the jobs in turn. The last two keep one stripe's cells in
+// flight at a time.
+constexpr int kJobsInLaunches = 1;
+constexpr int kJobsInKernel = 2;
+
 // One stripe (or one pass over a slice of a stripe's members):
 // out[j] (^)= sum_i coef[j][i] * in[i] over GF(2^8), byte by byte.
 struct GfJob {
@@ -31,6 +39,8 @@ struct GfLaunch {
   int accumulate;           // 0: out = sum, 1: out ^= sum
   int bytes_only;           // 1: a pointer is not 16-B aligned, use the byte path
   int blocks_per_job;
+  int sequential;           // job order: 0 side by side, kJobsInLaunches, kJobsInKernel (launch_gf)
+  int job0;                 // first job of this launch (set by the launcher)
   size_t nbytes;            // bytes per cell
 };
 
@@ -47,6 +57,8 @@ struct XorLaunch {
   int accumulate;
   int bytes_only;
   int blocks_per_job;
+  int sequential;
+  int job0;
   size_t nbytes;
 };
 

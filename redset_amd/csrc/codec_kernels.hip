@@ -52,13 +52,27 @@ int gf_blocks_per_cu(int nin) {
   return n;
 }
 
+// L.sequential (codec_kernels.h): kJobsInLaunches = the jobs go one after
+// another, one launch each on the whole grid, so only one stripe's ~11 cell
+// streams are in flight instead of every stripe's ~120: same bytes, fewer
+// concurrent DRAM streams (A/B in profiles/r01_sequential_jobs.txt);
+// kJobsInKernel = one launch on the whole grid whose blocks loop over the
+// jobs (codec_device.h); 0 = one launch, jobs side by side, blocks_per_job
+// blocks each.
 int launch_gf(const GfLaunch& L, void* stream) {
   if (L.nin < 1 || L.nin > kMaxIn || L.nout < 1 || L.nout > kMaxOut) return hipErrorInvalidValue;
   if (L.njobs == 0 || L.nbytes == 0) return hipSuccess;
-  const dim3 grid(static_cast<unsigned>(L.njobs * L.blocks_per_job));
-  hipLaunchKernelGGL(kernel_set(L.nin).gf[L.nout - 1][L.accumulate ? 1 : 0], grid, dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), L);
-  return hipGetLastError();
+  const GfKernel k = kernel_set(L.nin).gf[L.nout - 1][L.accumulate ? 1 : 0];
+  const int launches = L.sequential == kJobsInLaunches ? L.njobs : 1;
+  for (int j = 0; j < launches; ++j) {
+    GfLaunch one = L;
+    one.job0 = L.sequential ? j : 0;
+    const dim3 grid(static_cast<unsigned>((L.sequential ? 1 : L.njobs) * L.blocks_per_job));
+    hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), one);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 int launch_gf_single(const GfLaunch& L, const GfJob& J, void* stream) {
@@ -80,9 +94,17 @@ int launch_xor_single(const XorLaunch& L, const XorJob& J, void* stream) {
 int launch_xor(const XorLaunch& L, void* stream) {
   if (L.nin < 1 || L.nin > kMaxIn) return hipErrorInvalidValue;
   if (L.njobs == 0 || L.nbytes == 0) return hipSuccess;
-  const dim3 grid(static_cast<unsigned>(L.njobs * L.blocks_per_job));
-  hipLaunchKernelGGL(kernel_set(L.nin).xr[L.accumulate ? 1 : 0], grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), L);
-  return hipGetLastError();
+  const XorKernel k = kernel_set(L.nin).xr[L.accumulate ? 1 : 0];
+  const int launches = L.sequential == kJobsInLaunches ? L.njobs : 1;
+  for (int j = 0; j < launches; ++j) {
+    XorLaunch one = L;
+    one.job0 = L.sequential ? j : 0;
+    const dim3 grid(static_cast<unsigned>((L.sequential ? 1 : L.njobs) * L.blocks_per_job));
+    hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), one);
+    const hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  return hipSuccess;
 }
 
 }  // namespace redset_hip

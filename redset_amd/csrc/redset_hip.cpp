@@ -68,6 +68,28 @@ int target_blocks_per_cu(int occupancy) {
   return std::max(1, std::min(want, occupancy));
 }
 
+// Whether a plan runs the jobs of a launch one after another, each on the
+// whole grid (GfLaunch::sequential, launch_gf in codec_kernels.hip), instead
+// of side by side in one launch. Sequential keeps one stripe's ~11 cell
+// streams in flight instead of every stripe's ~120: +5-8% on the 64 MiB
+// RS(8+3) step (profiles/r01_sequential_jobs.txt). It costs one launch gap per
+// job, so it is used only when a job's cells are big enough to fill the grid
+// for much longer than that gap (>= kSequentialMinCell bytes per cell).
+// REDSET_HIP_SEQUENTIAL=0 / 1 forces it off / on (A/B, tests); read at every
+// plan build.
+constexpr size_t kSequentialMinCell = 16u << 20;
+
+// returns the launch's job order (codec_kernels.h): REDSET_HIP_SEQUENTIAL=0 /
+// 1 / 2 forces side by side / kJobsInLaunches / kJobsInKernel
+int sequential_jobs(int njobs, size_t nbytes) {
+  if (njobs < 2) return 0;
+  const char* s = std::getenv("REDSET_HIP_SEQUENTIAL");
+  if (s && s[0] >= '0' && s[0] <= '2' && s[1] == '\0') return s[0] - '0';
+  return nbytes >= kSequentialMinCell ? redset_hip::kJobsInLaunches : 0;
+}
+
+int launches_of(int order, int njobs) { return order == redset_hip::kJobsInLaunches ? njobs : 1; }
+
 // Blocks per job so the whole launch fits in one resident wave of blocks.
 int blocks_per_job(int njobs, size_t nbytes, int occupancy, int blocks_total = 0) {
   const long target = blocks_total > 0
@@ -170,7 +192,8 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     G.accumulate = P.accumulate;
     G.bytes_only = P.bytes_only;
     G.nbytes = nbytes;
-    G.blocks_per_job = blocks_per_job(G.njobs, nbytes, redset_hip::gf_blocks_per_cu(P.nin));
+    G.sequential = sequential_jobs(G.njobs, nbytes);
+    G.blocks_per_job = blocks_per_job(G.sequential ? 1 : G.njobs, nbytes, redset_hip::gf_blocks_per_cu(P.nin));
     gall.insert(gall.end(), P.jobs.begin(), P.jobs.end());
     plan->gf_launches.push_back(G);
   }
@@ -184,12 +207,15 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     X.accumulate = P.accumulate;
     X.bytes_only = P.bytes_only;
     X.nbytes = nbytes;
-    X.blocks_per_job = blocks_per_job(X.njobs, nbytes, 8);
+    X.sequential = sequential_jobs(X.njobs, nbytes);
+    X.blocks_per_job = blocks_per_job(X.sequential ? 1 : X.njobs, nbytes, 8);
     xall.insert(xall.end(), P.jobs.begin(), P.jobs.end());
     plan->xor_launches.push_back(X);
   }
   plan->info.jobs = static_cast<int>(gall.size() + xall.size());
-  plan->info.launches = static_cast<int>(plan->gf_launches.size() + plan->xor_launches.size());
+  plan->info.launches = 0;
+  for (const GfLaunch& G : plan->gf_launches) plan->info.launches += launches_of(G.sequential, G.njobs);
+  for (const XorLaunch& X : plan->xor_launches) plan->info.launches += launches_of(X.sequential, X.njobs);
   if (!gall.empty()) {
     if (int rc = hip_check(hipMalloc(&plan->d_gf, gall.size() * sizeof(GfJob)), "hipMalloc(plan jobs)")) return rc;
     if (int rc = hip_check(hipMemcpy(plan->d_gf, gall.data(), gall.size() * sizeof(GfJob), hipMemcpyHostToDevice),

@@ -191,3 +191,20 @@ def test_oracle_reproduces_golden(oracle, name):
         xorc = [np.zeros(chunk, np.uint8) for _ in range(p)]
         oracle.xor_encode_set(p, lofi, xorc, chunk)
         assert np.array_equal(np.stack(xorc), z["parity"])
+
+
+@pytest.mark.parametrize("name", ["rs_p11_e3_c64MiB", "xor_p8_c64MiB"])
+def test_full_size_inputs_regenerate(name):
+    """The full-size digest fixture (tests/golden/full_size_digests.json) is
+    usable: member 0's regenerated input hashes as recorded, and the recorded
+    case matches tests/full_size.py."""
+    import json
+
+    import full_size
+
+    with open(os.path.join(GOLDEN, "full_size_digests.json")) as f:
+        want = json.load(f)[name]
+    case = full_size.CASES[name]
+    assert all(want[k] == v for k, v in case.items())
+    assert len(want["parity_sha256"]) == case["ranks"]
+    assert full_size.sha256(full_size.member_lofi(case, 0)) == want["lofi_sha256"][0]

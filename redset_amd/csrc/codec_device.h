@@ -54,6 +54,21 @@
 #define REDSET_LOAD_POLICY 1
 #endif
 
+// Register budget of the kernels: N > 0 compiles them for at most N waves
+// per SIMD (amdgpu_waves_per_eu), i.e. up to 512 / N VGPRs; 0 lets the
+// compiler aim for 4 waves (<= 128 VGPRs). The codec runs 2 blocks of 4
+// waves per CU = 2 waves per SIMD (redset_hip.cpp), so 2 costs no occupancy;
+// it lets gf_mac<8,3> issue all 8 input loads of a position before its first
+// wait and measured +1.0% on the RS step (profiles/r01_ab_waves_per_eu.txt).
+#ifndef REDSET_WAVES_PER_EU
+#define REDSET_WAVES_PER_EU 2
+#endif
+#if REDSET_WAVES_PER_EU > 0
+#define REDSET_KERNEL __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, REDSET_WAVES_PER_EU)))
+#else
+#define REDSET_KERNEL __global__ void __launch_bounds__(kBlock)
+#endif
+
 namespace redset_hip {
 
 namespace {
@@ -359,7 +374,7 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
 // entry points: jobs from a device array (plans), or one job passed by
 // value in the kernel arguments (stripe primitives, no device descriptor)
 template <int NIN, int NOUT, bool ACC>
-__global__ void __launch_bounds__(kBlock) gf_mac_kernel(GfLaunch L) {
+REDSET_KERNEL gf_mac_kernel(GfLaunch L) {
   if (L.sequential == kJobsInKernel) {
     // every block sweeps every job in turn: one stripe's cells in flight at
     // a time, with no launch boundary between stripes
@@ -374,12 +389,12 @@ __global__ void __launch_bounds__(kBlock) gf_mac_kernel(GfLaunch L) {
 }
 
 template <int NIN, int NOUT, bool ACC>
-__global__ void __launch_bounds__(kBlock) gf_mac_kernel_arg(GfLaunch L, GfJob J) {
+REDSET_KERNEL gf_mac_kernel_arg(GfLaunch L, GfJob J) {
   gf_mac_body<NIN, NOUT, ACC>(L, J, blockIdx.x);
 }
 
 template <int NIN, bool ACC>
-__global__ void __launch_bounds__(kBlock) xor_kernel(XorLaunch L) {
+REDSET_KERNEL xor_kernel(XorLaunch L) {
   if (L.sequential == kJobsInKernel) {
     for (int j = 0; j < L.njobs; ++j) xor_body<NIN, ACC>(L, L.jobs[j], blockIdx.x);
     return;
@@ -389,7 +404,7 @@ __global__ void __launch_bounds__(kBlock) xor_kernel(XorLaunch L) {
 }
 
 template <int NIN, bool ACC>
-__global__ void __launch_bounds__(kBlock) xor_kernel_arg(XorLaunch L, XorJob J) {
+REDSET_KERNEL xor_kernel_arg(XorLaunch L, XorJob J) {
   xor_body<NIN, ACC>(L, J, blockIdx.x);
 }
 

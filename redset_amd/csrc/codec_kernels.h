@@ -16,9 +16,9 @@ constexpr int kMaxOut = 4;
 
 // Job order of a launch (GfLaunch / XorLaunch::sequential). 0: all jobs side
 // by side in one grid, blocks_per_job blocks each. kJobsInLaunches: one
-// launch per job over the whole grid. kJobsInKernel: one launch whose every
-// block sweeps the jobs in turn. The last two keep one stripe's cells in
-// flight at a time.
+// launch per job over the whole grid (or per `group` jobs side by side).
+// kJobsInKernel: one launch whose every block sweeps the jobs in turn. The
+// last two keep one stripe's cells in flight at a time.
 constexpr int kJobsInLaunches = 1;
 constexpr int kJobsInKernel = 2;
 
@@ -41,6 +41,7 @@ struct GfLaunch {
   int blocks_per_job;
   int sequential;           // job order: 0 side by side, kJobsInLaunches, kJobsInKernel (launch_gf)
   int job0;                 // first job of this launch (set by the launcher)
+  int group;                // kJobsInLaunches: jobs per launch, side by side (0 = 1)
   size_t nbytes;            // bytes per cell
 };
 
@@ -59,6 +60,7 @@ struct XorLaunch {
   int blocks_per_job;
   int sequential;
   int job0;
+  int group;
   size_t nbytes;
 };
 

@@ -2,6 +2,8 @@
 // themselves: codec_device.h, instantiated by codec_sets_*.hip).
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
+
 #include "codec_kernels.h"
 
 namespace redset_hip {
@@ -26,6 +28,12 @@ const KernelSet& kernel_set(int nin) {
     table[nin - 1] = s;
   }
   return *table[nin - 1];
+}
+
+// jobs one launch covers (the last launch may get fewer)
+template <class Launch>
+int jobs_per_launch(const Launch& L) {
+  return L.sequential == kJobsInLaunches ? std::max(1, L.group) : L.njobs;
 }
 
 }  // namespace
@@ -53,9 +61,9 @@ int gf_blocks_per_cu(int nin) {
 }
 
 // L.sequential (codec_kernels.h): kJobsInLaunches = the jobs go one after
-// another, one launch each on the whole grid, so only one stripe's ~11 cell
-// streams are in flight instead of every stripe's ~120: same bytes, fewer
-// concurrent DRAM streams (A/B in profiles/r01_sequential_jobs.txt);
+// another, one launch each on the whole grid (or L.group per launch), so
+// only one stripe's ~11 cell streams are in flight instead of every
+// stripe's ~120: same bytes, fewer concurrent DRAM streams (A/B in profiles/r01_sequential_jobs.txt);
 // kJobsInKernel = one launch on the whole grid whose blocks loop over the
 // jobs (codec_device.h); 0 = one launch, jobs side by side, blocks_per_job
 // blocks each.
@@ -63,11 +71,12 @@ int launch_gf(const GfLaunch& L, void* stream) {
   if (L.nin < 1 || L.nin > kMaxIn || L.nout < 1 || L.nout > kMaxOut) return hipErrorInvalidValue;
   if (L.njobs == 0 || L.nbytes == 0) return hipSuccess;
   const GfKernel k = kernel_set(L.nin).gf[L.nout - 1][L.accumulate ? 1 : 0];
-  const int launches = L.sequential == kJobsInLaunches ? L.njobs : 1;
-  for (int j = 0; j < launches; ++j) {
+  const int per = jobs_per_launch(L);
+  for (int j = 0; j < L.njobs; j += per) {
     GfLaunch one = L;
-    one.job0 = L.sequential ? j : 0;
-    const dim3 grid(static_cast<unsigned>((L.sequential ? 1 : L.njobs) * L.blocks_per_job));
+    one.job0 = j;
+    const int n = L.sequential == kJobsInKernel ? 1 : std::min(per, L.njobs - j);
+    const dim3 grid(static_cast<unsigned>(n * L.blocks_per_job));
     hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), one);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;
@@ -95,11 +104,12 @@ int launch_xor(const XorLaunch& L, void* stream) {
   if (L.nin < 1 || L.nin > kMaxIn) return hipErrorInvalidValue;
   if (L.njobs == 0 || L.nbytes == 0) return hipSuccess;
   const XorKernel k = kernel_set(L.nin).xr[L.accumulate ? 1 : 0];
-  const int launches = L.sequential == kJobsInLaunches ? L.njobs : 1;
-  for (int j = 0; j < launches; ++j) {
+  const int per = jobs_per_launch(L);
+  for (int j = 0; j < L.njobs; j += per) {
     XorLaunch one = L;
-    one.job0 = L.sequential ? j : 0;
-    const dim3 grid(static_cast<unsigned>((L.sequential ? 1 : L.njobs) * L.blocks_per_job));
+    one.job0 = j;
+    const int n = L.sequential == kJobsInKernel ? 1 : std::min(per, L.njobs - j);
+    const dim3 grid(static_cast<unsigned>(n * L.blocks_per_job));
     hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), one);
     const hipError_t e = hipGetLastError();
     if (e != hipSuccess) return e;

@@ -88,7 +88,21 @@ int sequential_jobs(int njobs, size_t nbytes) {
   return nbytes >= kSequentialMinCell ? redset_hip::kJobsInLaunches : 0;
 }
 
-int launches_of(int order, int njobs) { return order == redset_hip::kJobsInLaunches ? njobs : 1; }
+// Stripes per launch in sequence mode (side by side within the launch);
+// REDSET_HIP_STRIPES_PER_LAUNCH overrides the default of 1 (A/B).
+int stripes_per_launch() {
+  const char* s = std::getenv("REDSET_HIP_STRIPES_PER_LAUNCH");
+  return (s && std::atoi(s) > 0) ? std::atoi(s) : 1;
+}
+
+int launches_of(int order, int njobs, int group) {
+  return order == redset_hip::kJobsInLaunches ? (njobs + group - 1) / group : 1;
+}
+
+// jobs that share one launch's grid
+int jobs_sharing_grid(int order, int njobs, int group) {
+  return order == redset_hip::kJobsInLaunches ? std::min(group, njobs) : order == redset_hip::kJobsInKernel ? 1 : njobs;
+}
 
 // Blocks per job so the whole launch fits in one resident wave of blocks.
 int blocks_per_job(int njobs, size_t nbytes, int occupancy, int blocks_total = 0) {
@@ -193,7 +207,9 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     G.bytes_only = P.bytes_only;
     G.nbytes = nbytes;
     G.sequential = sequential_jobs(G.njobs, nbytes);
-    G.blocks_per_job = blocks_per_job(G.sequential ? 1 : G.njobs, nbytes, redset_hip::gf_blocks_per_cu(P.nin));
+    G.group = stripes_per_launch();
+    G.blocks_per_job = blocks_per_job(jobs_sharing_grid(G.sequential, G.njobs, G.group), nbytes,
+                                      redset_hip::gf_blocks_per_cu(P.nin));
     gall.insert(gall.end(), P.jobs.begin(), P.jobs.end());
     plan->gf_launches.push_back(G);
   }
@@ -208,14 +224,15 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     X.bytes_only = P.bytes_only;
     X.nbytes = nbytes;
     X.sequential = sequential_jobs(X.njobs, nbytes);
-    X.blocks_per_job = blocks_per_job(X.sequential ? 1 : X.njobs, nbytes, 8);
+    X.group = stripes_per_launch();
+    X.blocks_per_job = blocks_per_job(jobs_sharing_grid(X.sequential, X.njobs, X.group), nbytes, 8);
     xall.insert(xall.end(), P.jobs.begin(), P.jobs.end());
     plan->xor_launches.push_back(X);
   }
   plan->info.jobs = static_cast<int>(gall.size() + xall.size());
   plan->info.launches = 0;
-  for (const GfLaunch& G : plan->gf_launches) plan->info.launches += launches_of(G.sequential, G.njobs);
-  for (const XorLaunch& X : plan->xor_launches) plan->info.launches += launches_of(X.sequential, X.njobs);
+  for (const GfLaunch& G : plan->gf_launches) plan->info.launches += launches_of(G.sequential, G.njobs, G.group);
+  for (const XorLaunch& X : plan->xor_launches) plan->info.launches += launches_of(X.sequential, X.njobs, X.group);
   if (!gall.empty()) {
     if (int rc = hip_check(hipMalloc(&plan->d_gf, gall.size() * sizeof(GfJob)), "hipMalloc(plan jobs)")) return rc;
     if (int rc = hip_check(hipMemcpy(plan->d_gf, gall.data(), gall.size() * sizeof(GfJob), hipMemcpyHostToDevice),

@@ -253,18 +253,21 @@ def test_xor_encode_and_rebuild(rd, oracle, p, chunk, padded):
         assert np.array_equal(gl[root], lofi[root]) and np.array_equal(gp[root], xorc[root])
 
 
-@pytest.mark.parametrize("mode", ["0", "1", "2"])
-def test_plan_job_order(rd, oracle, monkeypatch, mode):
+@pytest.mark.parametrize("mode,group,n_rs,n_xor", [("0", "1", 1, 1), ("1", "1", 11, 8), ("1", "3", 4, 3),
+                                                   ("2", "1", 1, 1)])
+def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     """A plan runs its stripes side by side in one launch (REDSET_HIP_SEQUENTIAL=0),
-    one launch per stripe (=1, the default for cells >= 16 MiB) or one launch
-    whose blocks sweep the stripes in turn (=2): same bytes."""
+    one launch per stripe (=1, the default for cells >= 16 MiB; or per
+    REDSET_HIP_STRIPES_PER_LAUNCH stripes) or one launch whose blocks sweep the
+    stripes in turn (=2): same bytes."""
     monkeypatch.setenv("REDSET_HIP_SEQUENTIAL", mode)
+    monkeypatch.setenv("REDSET_HIP_STRIPES_PER_LAUNCH", group)
     p, e, chunk, lost = 11, 3, 40_000, [0, 5, 9]
     lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=41)
     lay = upload_set(rd, lofi, parity, p - e, e, chunk)
     codec = rd.RSCodec(p, e)
     enc = codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
-    assert enc.launches == (p if mode == "1" else 1)
+    assert enc.launches == n_rs
     enc.execute()
     torch.cuda.synchronize()
     oracle.OracleRS(p, e).encode_set(lofi, parity, chunk)
@@ -274,7 +277,7 @@ def test_plan_job_order(rd, oracle, monkeypatch, mode):
         lay.lofi(r).fill_(0xEE)
         lay.parity(r).fill_(0xEE)
     reb = codec.plan_rebuild(lost, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
-    assert reb.launches == (p if mode == "1" else 1)
+    assert reb.launches == n_rs
     reb.execute()
     torch.cuda.synchronize()
     gl, gp = download_set(lay)
@@ -283,7 +286,7 @@ def test_plan_job_order(rd, oracle, monkeypatch, mode):
     xl, xc = oracle.random_set(8, 7, 1, chunk, seed=42)
     xlay = upload_set(rd, xl, xc, 7, 1, chunk)
     xenc = rd.xor_plan_encode(8, xlay.lofi_ptrs(), xlay.parity_ptrs(), chunk, xlay.cell_stride)
-    assert xenc.launches == (8 if mode == "1" else 1)
+    assert xenc.launches == n_xor
     xenc.execute()
     torch.cuda.synchronize()
     oracle.xor_encode_set(8, xl, xc, chunk)

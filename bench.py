@@ -51,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
     ap.add_argument("--sharded", type=int, default=1, help="N>1: also time the RCCL sharded-rebuild leg")
     ap.add_argument("--xor", type=int, default=1, help="also time the XOR set of configs[1] (rank 0)")
+    ap.add_argument("--pairs", type=int, default=1,
+                    help="also time the rebuild of every pair of erased members (rank 0; SURVEY.md §8d worst case)")
     ap.add_argument("--dist-backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "traffic_latest.json"))
@@ -185,6 +187,40 @@ def copy_probe(stream, nbytes=1 << 30, reps=10):
         e1.record(stream)
     torch.cuda.synchronize()
     return round(2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
+
+
+def rebuild_pairs(codec, lay, chunk, stream, reps=5):
+    """configs[3] over every erasure pair: the rebuild rate of each 2-member
+    pattern on the bench's own set (event-timed, `reps` executes each after
+    one warm-up). The decode reads d survivors per stripe whatever the pair,
+    but which cells (data or parity) and their coefficients differ."""
+    import itertools
+
+    import torch
+
+    p = lay.ranks
+    rates = {}
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for pair in itertools.combinations(range(p), 2):
+        plan = codec.plan_rebuild(list(pair), lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+        plan.execute(stream)
+        e0.record(stream)
+        for _ in range(reps):
+            plan.execute(stream)
+        e1.record(stream)
+        torch.cuda.synchronize()
+        nbytes = plan.bytes_read + plan.bytes_written
+        rates[pair] = nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+        plan.close()
+    worst = min(rates, key=rates.get)
+    best = max(rates, key=rates.get)
+    vals = sorted(rates.values())
+    return {
+        "pairs": len(rates),
+        "min_GBps": round(rates[worst], 1), "worst_pair": list(worst),
+        "median_GBps": round(vals[len(vals) // 2], 1),
+        "max_GBps": round(rates[best], 1), "best_pair": list(best),
+    }
 
 
 def xor_leg(args, chunk, stream):
@@ -406,6 +442,8 @@ def main():
         "codec_vs_copy": round(achieved / box_copy, 4),
         "note": "same box, same process: device-to-device copy of 1 GiB (read + write bytes)",
     }
+    if args.pairs and rank == 0:
+        result["rebuild_every_pair"] = rebuild_pairs(codec, lay, chunk, stream)
     if args.xor and rank == 0:
         result["xor"] = xor_leg(args, chunk, stream)
     if dist_on and args.sharded:

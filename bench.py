@@ -189,28 +189,34 @@ def copy_probe(stream, nbytes=1 << 30, reps=10):
     return round(2 * nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9, 1)
 
 
-def rebuild_pairs(codec, lay, chunk, stream, reps=5):
+def rebuild_pairs(codec, lay, chunk, stream, reps=5, passes=2):
     """configs[3] over every erasure pair: the rebuild rate of each 2-member
-    pattern on the bench's own set (event-timed, `reps` executes each after
-    one warm-up). The decode reads d survivors per stripe whatever the pair,
-    but which cells (data or parity) and their coefficients differ."""
+    pattern on the bench's own set (event-timed, `reps` executes after one
+    warm-up, mean over `passes` sweeps; one pass alone leaves single pairs
+    up to 10% low by noise, profiles/r01_rebuild_pairs.txt). The decode reads
+    d survivors per stripe whatever the pair, but which cells (data or
+    parity) and their coefficients differ."""
     import itertools
 
     import torch
 
     p = lay.ranks
-    rates = {}
+    plans = {pair: codec.plan_rebuild(list(pair), lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+             for pair in itertools.combinations(range(p), 2)}
+    sums = dict.fromkeys(plans, 0.0)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    for pair in itertools.combinations(range(p), 2):
-        plan = codec.plan_rebuild(list(pair), lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
-        plan.execute(stream)
-        e0.record(stream)
-        for _ in range(reps):
+    for _ in range(passes):
+        for pair, plan in plans.items():
             plan.execute(stream)
-        e1.record(stream)
-        torch.cuda.synchronize()
-        nbytes = plan.bytes_read + plan.bytes_written
-        rates[pair] = nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+            e0.record(stream)
+            for _ in range(reps):
+                plan.execute(stream)
+            e1.record(stream)
+            torch.cuda.synchronize()
+            nbytes = plan.bytes_read + plan.bytes_written
+            sums[pair] += nbytes * reps / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    rates = {pair: v / passes for pair, v in sums.items()}
+    for plan in plans.values():
         plan.close()
     worst = min(rates, key=rates.get)
     best = max(rates, key=rates.get)

@@ -68,6 +68,20 @@ int target_blocks_per_cu(int occupancy) {
   return std::max(1, std::min(want, occupancy));
 }
 
+// Resident XOR blocks per CU. The XOR kernel has no tables and little VALU
+// work, so 4 waves per CU keep its 7 read streams busy with half the
+// requests in flight of the GF kernel's 8 waves: 6.00 vs 5.78 TB/s on the XOR
+// leg (profiles/r01_ab_xor_blocks.txt). REDSET_HIP_XOR_BLOCKS_PER_CU
+// overrides it (A/B).
+int xor_blocks_cap() {
+  static int env = -1;
+  if (env < 0) {
+    const char* s = std::getenv("REDSET_HIP_XOR_BLOCKS_PER_CU");
+    env = (s && std::atoi(s) > 0) ? std::atoi(s) : 1;
+  }
+  return env;
+}
+
 // Whether a plan runs the jobs of a launch one after another, each on the
 // whole grid (GfLaunch::sequential, launch_gf in codec_kernels.hip), instead
 // of side by side in one launch. Sequential keeps one stripe's ~11 cell
@@ -225,7 +239,7 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     X.nbytes = nbytes;
     X.sequential = sequential_jobs(X.njobs, nbytes);
     X.group = stripes_per_launch();
-    X.blocks_per_job = blocks_per_job(jobs_sharing_grid(X.sequential, X.njobs, X.group), nbytes, 8);
+    X.blocks_per_job = blocks_per_job(jobs_sharing_grid(X.sequential, X.njobs, X.group), nbytes, xor_blocks_cap());
     xall.insert(xall.end(), P.jobs.begin(), P.jobs.end());
     plan->xor_launches.push_back(X);
   }
@@ -307,7 +321,7 @@ int run_stripe(const StripeMap& m, const uint8_t* const* in, uint8_t* const* out
         X.accumulate = accumulate || ig > 0;
         X.bytes_only = al ? 0 : 1;
         X.nbytes = nbytes;
-        X.blocks_per_job = blocks_per_job(1, nbytes, 8, blocks_total);
+        X.blocks_per_job = blocks_per_job(1, nbytes, xor_blocks_cap(), blocks_total);
         e = launch_xor_single(X, J, stream);
       } else {
         GfJob J;
@@ -544,7 +558,7 @@ int redset_hip_xor_combine(const unsigned char* const* in, int nin, unsigned cha
   X.accumulate = accumulate ? 1 : 0;
   X.bytes_only = al ? 0 : 1;
   X.nbytes = nbytes;
-  X.blocks_per_job = blocks_per_job(1, nbytes, 8);
+  X.blocks_per_job = blocks_per_job(1, nbytes, xor_blocks_cap());
   return hip_check(static_cast<hipError_t>(redset_hip::launch_xor_single(X, J, stream)), "xor_combine launch");
 }
 

@@ -178,6 +178,42 @@ __device__ __forceinline__ void store_vec(g_u4* p, size_t v, v4u r) {
 #endif
 }
 
+// acc (packed partial products of all outputs, 16 bytes) ^= coef[.][i] * x
+__device__ __forceinline__ void gf_acc_input(const uint32_t* lds, const v4u& x, int i, uint32_t (&acc)[16]) {
+  const uint32_t w[4] = {x.x, x.y, x.z, x.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    // byte b of lo4 / hi4 = 4 * (low / high nibble of byte b) = table offset
+    const uint32_t lo4 = (w[q] << 2) & 0x3C3C3C3Cu;
+    const uint32_t hi4 = (w[q] >> 2) & 0x3C3C3C3Cu;
+    const uint32_t ol[4] = {byte_of<0>(lo4), byte_of<8>(lo4), byte_of<16>(lo4), byte_of<24>(lo4)};
+    const uint32_t oh[4] = {byte_of<0>(hi4), byte_of<8>(hi4), byte_of<16>(hi4), byte_of<24>(hi4)};
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+      acc[4 * q + b] = xor3(acc[4 * q + b], lds_at(lds, i * kTableBytes + ol[b]),
+                            lds_at(lds, i * kTableBytes + 64 + oh[b]));
+    }
+  }
+}
+
+// transpose the packed accumulators back to per-output bytes and store
+template <int NOUT, bool ACC>
+__device__ __forceinline__ void gf_finish(const uint32_t (&acc)[16], g_u4* const (&out)[NOUT], size_t v, bool store) {
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j) {
+    v4u r;
+    r.x = gather_byte(acc[0], acc[1], acc[2], acc[3], j);
+    r.y = gather_byte(acc[4], acc[5], acc[6], acc[7], j);
+    r.z = gather_byte(acc[8], acc[9], acc[10], acc[11], j);
+    r.w = gather_byte(acc[12], acc[13], acc[14], acc[15], j);
+    if constexpr (ACC) {
+      if (store) out[j][v] = r ^ out[j][v];
+    } else {
+      store_vec(out[j], v, r);
+    }
+  }
+}
+
 // out[j][v] (^)= sum_i coef[j][i] * x[i] for one 16-B position of every cell
 template <int NIN, int NOUT, bool ACC>
 __device__ __forceinline__ void gf_mac_vec(const uint32_t* lds, const v4u (&x)[NIN], g_u4* const (&out)[NOUT],
@@ -202,35 +238,8 @@ __device__ __forceinline__ void gf_mac_vec(const uint32_t* lds, const v4u (&x)[N
 #pragma unroll
   for (int b = 0; b < 16; ++b) acc[b] = 0;
 #pragma unroll
-  for (int i = 0; i < NIN; ++i) {
-    const uint32_t w[4] = {x[i].x, x[i].y, x[i].z, x[i].w};
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      // byte b of lo4 / hi4 = 4 * (low / high nibble of byte b) = table offset
-      const uint32_t lo4 = (w[q] << 2) & 0x3C3C3C3Cu;
-      const uint32_t hi4 = (w[q] >> 2) & 0x3C3C3C3Cu;
-      const uint32_t ol[4] = {byte_of<0>(lo4), byte_of<8>(lo4), byte_of<16>(lo4), byte_of<24>(lo4)};
-      const uint32_t oh[4] = {byte_of<0>(hi4), byte_of<8>(hi4), byte_of<16>(hi4), byte_of<24>(hi4)};
-#pragma unroll
-      for (int b = 0; b < 4; ++b) {
-        acc[4 * q + b] = xor3(acc[4 * q + b], lds_at(lds, i * kTableBytes + ol[b]),
-                              lds_at(lds, i * kTableBytes + 64 + oh[b]));
-      }
-    }
-  }
-#pragma unroll
-  for (int j = 0; j < NOUT; ++j) {
-    v4u r;
-    r.x = gather_byte(acc[0], acc[1], acc[2], acc[3], j);
-    r.y = gather_byte(acc[4], acc[5], acc[6], acc[7], j);
-    r.z = gather_byte(acc[8], acc[9], acc[10], acc[11], j);
-    r.w = gather_byte(acc[12], acc[13], acc[14], acc[15], j);
-    if constexpr (ACC) {
-      if (store) out[j][v] = r ^ out[j][v];
-    } else {
-      store_vec(out[j], v, r);
-    }
-  }
+  for (int i = 0; i < NIN; ++i) gf_acc_input(lds, x[i], i, acc);
+  gf_finish<NOUT, ACC>(acc, out, v, store);
 }
 
 template <int NIN, bool ACC>

@@ -27,15 +27,15 @@ ok $s || exit $s
 
 echo "== rocprofv3 kernel stats" | tee -a "$OUT/progress.txt"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-  python3 bench.py --steps 20 --warmup 3 --cpu-baseline 0 > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+  python3 bench.py --steps 20 --warmup 3 --cpu-baseline 0 --pairs 0 > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 s=$?; echo "rocprof exit $s" | tee -a "$OUT/progress.txt"
 ok $s || exit $s
 echo "== rocprofv3 PMC FETCH_SIZE / WRITE_SIZE (separate passes)" | tee -a "$OUT/progress.txt"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o fetch -- \
-  python3 bench.py --steps 4 --warmup 1 --cpu-baseline 0 > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
+  python3 bench.py --steps 4 --warmup 1 --cpu-baseline 0 --pairs 0 > "$OUT/pmc_fetch.json" 2> "$OUT/pmc_fetch.err"
 s=$?; echo "pmc fetch exit $s" | tee -a "$OUT/progress.txt"; ok $s || exit $s
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_write" -o write -- \
-  python3 bench.py --steps 4 --warmup 1 --cpu-baseline 0 > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
+  python3 bench.py --steps 4 --warmup 1 --cpu-baseline 0 --pairs 0 > "$OUT/pmc_write.json" 2> "$OUT/pmc_write.err"
 s=$?; echo "pmc write exit $s" | tee -a "$OUT/progress.txt"; ok $s || exit $s
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/traffic.json" > /dev/null
 echo "== done" | tee -a "$OUT/progress.txt"

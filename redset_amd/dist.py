@@ -372,12 +372,27 @@ class ShardedSetRunner:
     def report(self, step_seconds: float, op: str = "step") -> dict:
         coll = {"encode": "RCCL all_to_all (data slices, then parity slices)",
                 "rebuild": "batched RCCL P2P: decode inputs' slices in, rebuilt slices back to their hosts"}
-        return {
+        phases = self.phase_ms() if self.timing else None
+        out = {
             "exchange": {
                 "bytes_sent_per_gpu_per_step": self.exchanged_bytes(op),
                 "column_slice_bytes": self.W,
                 "collective": coll.get(op, coll["encode"] + "; " + coll["rebuild"]),
-                "phase_ms_rank0": self.phase_ms() if self.timing else None,
+                "phase_ms_rank0": phases,
             },
             "per_gpu_GBps": round(self.algorithmic_bytes(op) / step_seconds / 1e9, 2),
         }
+        if phases and op == "rebuild" and self.world > 1:
+            # rank 0's send rate over the fabric in each exchange phase (what
+            # bounds the sharded rebuild; compare with xGMI, 7 links per GPU)
+            if self._gather_ops is None:
+                self._build_rebuild_gather()
+            if self._return_ops is None:
+                self._build_return()
+            g_ms = phases.get("rebuild_start->gathered")
+            r_ms = phases.get("rebuild_computed->done")
+            out["exchange"]["gather_send_GBps_rank0"] = (round(self._gather_sent / (g_ms * 1e-3) / 1e9, 1)
+                                                         if g_ms else None)
+            out["exchange"]["return_send_GBps_rank0"] = (round(self._return_sent / (r_ms * 1e-3) / 1e9, 1)
+                                                         if r_ms and self._return_sent else None)
+        return out

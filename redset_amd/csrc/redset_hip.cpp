@@ -82,19 +82,18 @@ int xor_blocks_cap() {
   return env;
 }
 
-// Whether a plan runs the jobs of a launch one after another, each on the
-// whole grid (GfLaunch::sequential, launch_gf in codec_kernels.hip), instead
-// of side by side in one launch. Sequential keeps one stripe's ~11 cell
-// streams in flight instead of every stripe's ~120: +5-8% on the 64 MiB
-// RS(8+3) step (profiles/r01_sequential_jobs.txt). It costs one launch gap per
-// job, so it is used only when a job's cells are big enough to fill the grid
-// for much longer than that gap (>= kSequentialMinCell bytes per cell).
-// REDSET_HIP_SEQUENTIAL=0 / 1 forces it off / on (A/B, tests); read at every
-// plan build.
+// Job order of a plan's launches (codec_kernels.h). Stripes in sequence, one
+// launch each over the whole grid (kJobsInLaunches), keep one stripe's ~11
+// cell streams in flight instead of every stripe's ~120: +6.5% on the 64 MiB
+// RS(8+3) step; two or three stripes per launch cost 3% / 6%, and one launch
+// looping over the stripes (kJobsInKernel) 5% (profiles/r01_sequential_jobs.txt).
+// A launch per stripe costs a launch boundary, so it is used only when a
+// stripe's cells are big enough to fill the grid for much longer than that
+// (>= kSequentialMinCell bytes per cell); smaller sets keep their stripes side
+// by side in one launch (0). REDSET_HIP_SEQUENTIAL=0 / 1 / 2 forces an order
+// (A/B, tests); read at every plan build.
 constexpr size_t kSequentialMinCell = 16u << 20;
 
-// returns the launch's job order (codec_kernels.h): REDSET_HIP_SEQUENTIAL=0 /
-// 1 / 2 forces side by side / kJobsInLaunches / kJobsInKernel
 int sequential_jobs(int njobs, size_t nbytes) {
   if (njobs < 2) return 0;
   const char* s = std::getenv("REDSET_HIP_SEQUENTIAL");

@@ -87,12 +87,14 @@ int xor_blocks_cap() {
 // cell streams in flight instead of every stripe's ~120: +6.5% on the 64 MiB
 // RS(8+3) step; two or three stripes per launch cost 3% / 6%, and one launch
 // looping over the stripes (kJobsInKernel) 5% (profiles/r01_sequential_jobs.txt).
-// A launch per stripe costs a launch boundary, so it is used only when a
-// stripe's cells are big enough to fill the grid for much longer than that
-// (>= kSequentialMinCell bytes per cell); smaller sets keep their stripes side
-// by side in one launch (0). REDSET_HIP_SEQUENTIAL=0 / 1 / 2 forces an order
-// (A/B, tests); read at every plan build.
-constexpr size_t kSequentialMinCell = 16u << 20;
+// Each launch pays a ramp-up and a drain, so sequence only pays for big cells:
+// side by side wins at 16 MiB cells (5.30 vs 5.14 TB/s), sequence at 24 MiB
+// (5.43 vs 5.16) and 32 MiB (5.46 vs 5.11); grouping 2-6 stripes per launch
+// never beats both (profiles/r01_sequential_jobs.txt, cell-size sweeps). Sets
+// with smaller cells keep their stripes side by side in one launch (0).
+// REDSET_HIP_SEQUENTIAL=0 / 1 / 2 forces an order (A/B, tests); read at every
+// plan build.
+constexpr size_t kSequentialMinCell = 24u << 20;
 
 int sequential_jobs(int njobs, size_t nbytes) {
   if (njobs < 2) return 0;

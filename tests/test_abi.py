@@ -163,3 +163,41 @@ def test_shape_and_error_recording(hiplib):
     L.redset_hip_rs_destroy(h)
     assert L.redset_hip_record_error(b"per-rank backend: lofi read failed") == 1
     assert L.redset_hip_last_error() == b"per-rank backend: lofi read failed"
+
+
+def test_bad_arguments_rejected_before_any_device_work(hiplib):
+    """Argument checks of the C ABI fail with REDSET_FAILURE and a message
+    before touching the device (runs on CPU): erasure lists out of range, not
+    ascending, duplicated or longer than the parity count (src/redset_
+    reedsolomon.c:1096), and malformed stripe-primitive calls."""
+    from ctypes import POINTER, byref, c_int, c_ubyte, c_void_p
+
+    from redset_amd import _lib
+
+    L = _lib.load()
+    h = c_void_p()
+    assert L.redset_hip_rs_create(11, 3, byref(h)) == 0
+    out = (c_ubyte * (4 * 11))()
+    for ranks, msg in [([11], b"out of range"), ([-1], b"out of range"), ([2, 1], b"ascending"),
+                       ([3, 3], b"ascending"), ([0, 1, 2, 3], b"cannot rebuild")]:
+        arr = (c_int * len(ranks))(*ranks)
+        assert L.redset_hip_rs_decode_matrix(h, len(ranks), arr, 0, out) == 1, ranks
+        assert msg in L.redset_hip_last_error(), (ranks, L.redset_hip_last_error())
+    L.redset_hip_rs_destroy(h)
+    ptrs = (c_void_p * 2)(16, 32)
+    nul = (c_void_p * 2)(16, None)
+    coef = (c_ubyte * 4)(1, 2, 3, 4)
+    PP = POINTER(c_void_p)
+    as_pp = lambda a: ctypes.cast(a, PP)  # noqa: E731
+    assert L.redset_hip_gf_combine(as_pp(ptrs), 0, as_pp(ptrs), 1, coef, 64, 0, None) == 1
+    assert b"nin=0" in L.redset_hip_last_error()
+    assert L.redset_hip_gf_combine(as_pp(ptrs), 257, as_pp(ptrs), 1, coef, 64, 0, None) == 1
+    assert L.redset_hip_gf_combine(as_pp(nul), 2, as_pp(ptrs), 1, coef, 64, 0, None) == 1
+    assert b"null input 1" in L.redset_hip_last_error()
+    assert L.redset_hip_gf_combine(as_pp(ptrs), 2, as_pp(nul), 2, coef, 64, 0, None) == 1
+    assert b"null output 1" in L.redset_hip_last_error()
+    assert L.redset_hip_gf_combine(None, 2, as_pp(ptrs), 1, coef, 64, 0, None) == 1
+    assert L.redset_hip_xor_combine(as_pp(ptrs), 0, 16, 64, 0, None) == 1
+    assert L.redset_hip_xor_combine(as_pp(nul), 2, 16, 64, 0, None) == 1
+    assert b"null input 1" in L.redset_hip_last_error()
+    assert L.redset_hip_xor_combine(as_pp(ptrs), 2, None, 64, 0, None) == 1

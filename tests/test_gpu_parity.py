@@ -294,6 +294,25 @@ def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     assert all(np.array_equal(a, b) for a, b in zip(xgot, xc))
 
 
+def test_zero_length_calls_are_noops(rd):
+    """Zero-byte stripe primitives and zero-chunk plans succeed without
+    touching their outputs (redset never makes a chunk smaller than 1 byte,
+    src/redset_reedsolomon.c:491-493, but the ABI accepts 0)."""
+    ins = [torch.full((64,), i + 1, dtype=torch.uint8, device="cuda") for i in range(3)]
+    outs = [torch.full((64,), 0xAB, dtype=torch.uint8, device="cuda") for _ in range(2)]
+    rd.gf_combine(ins, outs, np.ones((2, 3), np.uint8), 0)
+    rd.xor_combine(ins, outs[0], 0)
+    lay = rd.SetLayout.allocate(6, 4, 2, 256)
+    lay.storage.fill_(0xCD)
+    codec = rd.RSCodec(6, 2)
+    codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), 0, lay.cell_stride).execute()
+    codec.plan_rebuild([1, 4], lay.lofi_ptrs(), lay.parity_ptrs(), 0, lay.cell_stride).execute()
+    rd.xor_plan_encode(6, lay.lofi_ptrs(), lay.parity_ptrs(), 0, lay.cell_stride).execute()
+    torch.cuda.synchronize()
+    assert all(bool((o == 0xAB).all()) for o in outs)
+    assert bool((lay.storage == 0xCD).all())
+
+
 def test_plan_replays_in_cuda_graph(rd, oracle):
     p, e, chunk = 11, 3, 1 << 16
     lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=5)

@@ -41,6 +41,15 @@
 #ifndef REDSET_MEMONLY
 #define REDSET_MEMONLY 0
 #endif
+// Table offsets of the GF lookups: 0 = packed shift + mask, then one extract
+// per offset (12 VALU ops per input dword); 1 = one SDWA-byte-select AND per
+// offset (10 ops); 2 (default) = SDWA only in kernels with <= 2 outputs. The
+// fixed per-position cost weighs most where few output bytes amortise it:
+// SDWA gains 3.8% on the 2-output rebuild and loses 0.6% on the 3-output
+// encode, so 2 = +1.9% on the RS step (profiles/r01_ab_sdwa_offsets.txt).
+#ifndef REDSET_SDWA_OFFSETS
+#define REDSET_SDWA_OFFSETS 2
+#endif
 // Cache policy of the cell streams. Every cell byte is read or written
 // exactly once, so both directions are marked non-temporal (`nt`): +3% on
 // the RS step and +7% on XOR against the default policy, while either one
@@ -116,6 +125,22 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t x) {
   }
 }
 
+// 4 * (nibble of byte B of x >> or << 2) in one VALU op: v_and_b32 with an
+// SDWA byte select on x (x = w << 2: low nibble of byte B of w; x = w >> 2:
+// its high nibble), 60 = 0x3C keeps the four nibble bits at offset 2
+constexpr bool use_sdwa_offsets(int nout) {
+  return REDSET_SDWA_OFFSETS == 1 || (REDSET_SDWA_OFFSETS == 2 && nout <= 2);
+}
+
+template <int B>
+__device__ __forceinline__ uint32_t nibble_offset(uint32_t x) {
+  uint32_t r;
+  asm("v_and_b32_sdwa %0, 60, %1 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_%2"
+      : "=v"(r)
+      : "v"(x), "i"(B));
+  return r;
+}
+
 // a ^ b ^ c in one VALU op (v_bitop3_b32, truth table 0x96); gfx950 has no
 // v_xor3_b32 and hipcc does not form bitop3 from plain XORs
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -178,16 +203,28 @@ __device__ __forceinline__ void store_vec(g_u4* p, size_t v, v4u r) {
 #endif
 }
 
-// acc (packed partial products of all outputs, 16 bytes) ^= coef[.][i] * x
+// acc (packed partial products of all outputs, 16 bytes) ^= coef[.][i] * x;
+// SDWA: table offsets by SDWA byte selects (see REDSET_SDWA_OFFSETS)
+template <bool SDWA>
 __device__ __forceinline__ void gf_acc_input(const uint32_t* lds, const v4u& x, int i, uint32_t (&acc)[16]) {
   const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
-    // byte b of lo4 / hi4 = 4 * (low / high nibble of byte b) = table offset
-    const uint32_t lo4 = (w[q] << 2) & 0x3C3C3C3Cu;
-    const uint32_t hi4 = (w[q] >> 2) & 0x3C3C3C3Cu;
-    const uint32_t ol[4] = {byte_of<0>(lo4), byte_of<8>(lo4), byte_of<16>(lo4), byte_of<24>(lo4)};
-    const uint32_t oh[4] = {byte_of<0>(hi4), byte_of<8>(hi4), byte_of<16>(hi4), byte_of<24>(hi4)};
+    uint32_t ol[4], oh[4];
+    if constexpr (SDWA) {
+      // one SDWA op per table offset: 10 VALU ops per dword instead of 12
+      const uint32_t wl = w[q] << 2, wh = w[q] >> 2;
+      ol[0] = nibble_offset<0>(wl), ol[1] = nibble_offset<1>(wl), ol[2] = nibble_offset<2>(wl);
+      ol[3] = nibble_offset<3>(wl);
+      oh[0] = nibble_offset<0>(wh), oh[1] = nibble_offset<1>(wh), oh[2] = nibble_offset<2>(wh);
+      oh[3] = nibble_offset<3>(wh);
+    } else {
+      // byte b of lo4 / hi4 = 4 * (low / high nibble of byte b) = table offset
+      const uint32_t lo4 = (w[q] << 2) & 0x3C3C3C3Cu;
+      const uint32_t hi4 = (w[q] >> 2) & 0x3C3C3C3Cu;
+      ol[0] = byte_of<0>(lo4), ol[1] = byte_of<8>(lo4), ol[2] = byte_of<16>(lo4), ol[3] = byte_of<24>(lo4);
+      oh[0] = byte_of<0>(hi4), oh[1] = byte_of<8>(hi4), oh[2] = byte_of<16>(hi4), oh[3] = byte_of<24>(hi4);
+    }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       acc[4 * q + b] = xor3(acc[4 * q + b], lds_at(lds, i * kTableBytes + ol[b]),
@@ -238,7 +275,7 @@ __device__ __forceinline__ void gf_mac_vec(const uint32_t* lds, const v4u (&x)[N
 #pragma unroll
   for (int b = 0; b < 16; ++b) acc[b] = 0;
 #pragma unroll
-  for (int i = 0; i < NIN; ++i) gf_acc_input(lds, x[i], i, acc);
+  for (int i = 0; i < NIN; ++i) gf_acc_input<use_sdwa_offsets(NOUT)>(lds, x[i], i, acc);
   gf_finish<NOUT, ACC>(acc, out, v, store);
 }
 

@@ -95,18 +95,30 @@ __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
   return r;
 }
 
-// LDS image: [input][half][nibble] dwords = 128 B per input.
-constexpr int kTableBytes = 2 * 16 * 4;
+// LDS image per input: the low-nibble table (16 dwords, entry n at byte 4n)
+// then the high-nibble table at kHiBase with entries kHiStride bytes apart.
+// Stride 16 makes byte k of (w & 0xF0F0F0F0) the high table's offset as is,
+// one op per input dword fewer than (w >> 2) & 0x3C3C3C3C, but measured 2.8%
+// slower on the rebuild (profiles/r01_ab_sdwa_offsets.txt), so 4 stays (A/B
+// knob; both strides keep the 16 entries in 16 distinct LDS banks).
+#ifndef REDSET_HI_STRIDE
+#define REDSET_HI_STRIDE 4
+#endif
+constexpr int kHiStride = REDSET_HI_STRIDE;
+constexpr int kHiBase = 16 * 4;
+constexpr int kTableBytes = kHiBase + 16 * kHiStride;
 
 __device__ __forceinline__ void build_tables(uint32_t* lds, const GfJob& J, int nin, int nout) {
   const int entries = nin * 32;  // (input, half, nibble)
   for (int e = threadIdx.x; e < entries; e += blockDim.x) {
     const int i = e >> 5;
     const int h = (e >> 4) & 1;
-    const uint32_t x = static_cast<uint32_t>(e & 15) << (4 * h);
+    const int n = e & 15;
+    const uint32_t x = static_cast<uint32_t>(n) << (4 * h);
     uint32_t v = 0;
     for (int j = 0; j < nout; ++j) v |= gf_mul_dev(J.coef[j][i], x) << (8 * j);
-    lds[e] = v;
+    const int off = i * kTableBytes + (h ? kHiBase + n * kHiStride : n * 4);
+    *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + off) = v;
   }
 }
 
@@ -130,6 +142,16 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t x) {
 // its high nibble), 60 = 0x3C keeps the four nibble bits at offset 2
 constexpr bool use_sdwa_offsets(int nout) {
   return REDSET_SDWA_OFFSETS == 1 || (REDSET_SDWA_OFFSETS == 2 && nout <= 2);
+}
+
+// byte B of x & mask (an SGPR) in one op, the same SDWA form
+template <int B>
+__device__ __forceinline__ uint32_t byte_and(uint32_t x, uint32_t mask) {
+  uint32_t r;
+  asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_%3"
+      : "=v"(r)
+      : "s"(mask), "v"(x), "i"(B));
+  return r;
 }
 
 template <int B>
@@ -213,22 +235,28 @@ __device__ __forceinline__ void gf_acc_input(const uint32_t* lds, const v4u& x, 
     uint32_t ol[4], oh[4];
     if constexpr (SDWA) {
       // one SDWA op per table offset: 10 VALU ops per dword instead of 12
-      const uint32_t wl = w[q] << 2, wh = w[q] >> 2;
+      const uint32_t wl = w[q] << 2;
       ol[0] = nibble_offset<0>(wl), ol[1] = nibble_offset<1>(wl), ol[2] = nibble_offset<2>(wl);
       ol[3] = nibble_offset<3>(wl);
-      oh[0] = nibble_offset<0>(wh), oh[1] = nibble_offset<1>(wh), oh[2] = nibble_offset<2>(wh);
-      oh[3] = nibble_offset<3>(wh);
+      if constexpr (kHiStride == 16) {
+        oh[0] = byte_and<0>(w[q], 0xF0u), oh[1] = byte_and<1>(w[q], 0xF0u), oh[2] = byte_and<2>(w[q], 0xF0u);
+        oh[3] = byte_and<3>(w[q], 0xF0u);
+      } else {
+        const uint32_t wh = w[q] >> 2;
+        oh[0] = nibble_offset<0>(wh), oh[1] = nibble_offset<1>(wh), oh[2] = nibble_offset<2>(wh);
+        oh[3] = nibble_offset<3>(wh);
+      }
     } else {
       // byte b of lo4 / hi4 = 4 * (low / high nibble of byte b) = table offset
       const uint32_t lo4 = (w[q] << 2) & 0x3C3C3C3Cu;
-      const uint32_t hi4 = (w[q] >> 2) & 0x3C3C3C3Cu;
+      const uint32_t hi4 = kHiStride == 16 ? (w[q] & 0xF0F0F0F0u) : ((w[q] >> 2) & 0x3C3C3C3Cu);
       ol[0] = byte_of<0>(lo4), ol[1] = byte_of<8>(lo4), ol[2] = byte_of<16>(lo4), ol[3] = byte_of<24>(lo4);
       oh[0] = byte_of<0>(hi4), oh[1] = byte_of<8>(hi4), oh[2] = byte_of<16>(hi4), oh[3] = byte_of<24>(hi4);
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       acc[4 * q + b] = xor3(acc[4 * q + b], lds_at(lds, i * kTableBytes + ol[b]),
-                            lds_at(lds, i * kTableBytes + 64 + oh[b]));
+                            lds_at(lds, i * kTableBytes + kHiBase + oh[b]));
     }
   }
 }
@@ -382,7 +410,7 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
 #pragma unroll
     for (int i = 0; i < NIN; ++i) {
       const uint32_t b = J.in[i][k];
-      acc ^= lds[i * 32 + (b & 15u)] ^ lds[i * 32 + 16 + (b >> 4)];
+      acc ^= lds_at(lds, i * kTableBytes + (b & 15u) * 4) ^ lds_at(lds, i * kTableBytes + kHiBase + (b >> 4) * kHiStride);
     }
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) {

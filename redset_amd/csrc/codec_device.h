@@ -50,6 +50,10 @@
 #ifndef REDSET_SDWA_OFFSETS
 #define REDSET_SDWA_OFFSETS 2
 #endif
+// knob 2: the SDWA parts (sdwa_parts) of the kernels with > 2 outputs
+#ifndef REDSET_SDWA_WIDE_PARTS
+#define REDSET_SDWA_WIDE_PARTS 0
+#endif
 // Cache policy of the cell streams. Every cell byte is read or written
 // exactly once, so both directions are marked non-temporal (`nt`): +3% on
 // the RS step and +7% on XOR against the default policy, while either one
@@ -140,8 +144,10 @@ __device__ __forceinline__ uint32_t byte_of(uint32_t x) {
 // 4 * (nibble of byte B of x >> or << 2) in one VALU op: v_and_b32 with an
 // SDWA byte select on x (x = w << 2: low nibble of byte B of w; x = w >> 2:
 // its high nibble), 60 = 0x3C keeps the four nibble bits at offset 2
-constexpr bool use_sdwa_offsets(int nout) {
-  return REDSET_SDWA_OFFSETS == 1 || (REDSET_SDWA_OFFSETS == 2 && nout <= 2);
+// which table offsets a kernel with `nout` outputs computes by SDWA:
+// bit 0 = low-nibble offsets, bit 1 = high-nibble offsets
+constexpr int sdwa_parts(int nout) {
+  return REDSET_SDWA_OFFSETS == 1 ? 3 : REDSET_SDWA_OFFSETS == 2 ? (nout <= 2 ? 3 : REDSET_SDWA_WIDE_PARTS) : 0;
 }
 
 // byte B of x & mask (an SGPR) in one op, the same SDWA form
@@ -227,17 +233,23 @@ __device__ __forceinline__ void store_vec(g_u4* p, size_t v, v4u r) {
 
 // acc (packed partial products of all outputs, 16 bytes) ^= coef[.][i] * x;
 // SDWA: table offsets by SDWA byte selects (see REDSET_SDWA_OFFSETS)
-template <bool SDWA>
+template <int SDWA>
 __device__ __forceinline__ void gf_acc_input(const uint32_t* lds, const v4u& x, int i, uint32_t (&acc)[16]) {
   const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     uint32_t ol[4], oh[4];
-    if constexpr (SDWA) {
-      // one SDWA op per table offset: 10 VALU ops per dword instead of 12
+    if constexpr ((SDWA & 1) != 0) {
+      // one SDWA op per table offset instead of 1.5
       const uint32_t wl = w[q] << 2;
       ol[0] = nibble_offset<0>(wl), ol[1] = nibble_offset<1>(wl), ol[2] = nibble_offset<2>(wl);
       ol[3] = nibble_offset<3>(wl);
+    } else {
+      // byte b of lo4 = 4 * (low nibble of byte b) = table offset
+      const uint32_t lo4 = (w[q] << 2) & 0x3C3C3C3Cu;
+      ol[0] = byte_of<0>(lo4), ol[1] = byte_of<8>(lo4), ol[2] = byte_of<16>(lo4), ol[3] = byte_of<24>(lo4);
+    }
+    if constexpr ((SDWA & 2) != 0) {
       if constexpr (kHiStride == 16) {
         oh[0] = byte_and<0>(w[q], 0xF0u), oh[1] = byte_and<1>(w[q], 0xF0u), oh[2] = byte_and<2>(w[q], 0xF0u);
         oh[3] = byte_and<3>(w[q], 0xF0u);
@@ -247,10 +259,7 @@ __device__ __forceinline__ void gf_acc_input(const uint32_t* lds, const v4u& x, 
         oh[3] = nibble_offset<3>(wh);
       }
     } else {
-      // byte b of lo4 / hi4 = 4 * (low / high nibble of byte b) = table offset
-      const uint32_t lo4 = (w[q] << 2) & 0x3C3C3C3Cu;
       const uint32_t hi4 = kHiStride == 16 ? (w[q] & 0xF0F0F0F0u) : ((w[q] >> 2) & 0x3C3C3C3Cu);
-      ol[0] = byte_of<0>(lo4), ol[1] = byte_of<8>(lo4), ol[2] = byte_of<16>(lo4), ol[3] = byte_of<24>(lo4);
       oh[0] = byte_of<0>(hi4), oh[1] = byte_of<8>(hi4), oh[2] = byte_of<16>(hi4), oh[3] = byte_of<24>(hi4);
     }
 #pragma unroll
@@ -303,7 +312,7 @@ __device__ __forceinline__ void gf_mac_vec(const uint32_t* lds, const v4u (&x)[N
 #pragma unroll
   for (int b = 0; b < 16; ++b) acc[b] = 0;
 #pragma unroll
-  for (int i = 0; i < NIN; ++i) gf_acc_input<use_sdwa_offsets(NOUT)>(lds, x[i], i, acc);
+  for (int i = 0; i < NIN; ++i) gf_acc_input<sdwa_parts(NOUT)>(lds, x[i], i, acc);
   gf_finish<NOUT, ACC>(acc, out, v, store);
 }
 

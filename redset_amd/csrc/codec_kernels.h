@@ -75,7 +75,11 @@ int device_cu_count();
 // occupancy of the GF kernel for a given input count (blocks per CU)
 int gf_blocks_per_cu(int nin);
 
-constexpr int kBlock = 256;
+#ifndef REDSET_BLOCK
+#define REDSET_BLOCK 512
+#endif
+// threads per block (A/B knob: 512 = one block per CU at the same waves per CU)
+constexpr int kBlock = REDSET_BLOCK;
 
 // The kernels of one input count: [nout - 1][accumulate] for gf_mac,
 // [accumulate] for xor_reduce; *_arg take the job by value.

@@ -53,10 +53,11 @@ int hip_check(hipError_t e, const char* what) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// Resident 256-thread blocks per CU the codec aims for. HBM streams best at
-// low occupancy here: 2 blocks (8 waves, 64 KiB of loads in flight) per CU
-// beat 1, 3, 4 and 8 on every box measured (tools/bpc_sweep.sh,
-// profiles/r01_ab_pipeline.txt; 1 block starves the channels, more add DRAM
+// Resident blocks per CU the codec aims for: 8 waves per CU (2 blocks of 256
+// threads or 1 of 512). HBM streams best at low occupancy here: 8 waves
+// (64 KiB of loads in flight) per CU beat 4, 12, 16 and 32 on every box
+// measured (tools/bpc_sweep.sh, profiles/r01_ab_pipeline.txt,
+// r01_ab_waves_per_eu.txt; 4 waves leave the lookups uncovered, more add DRAM
 // row contention); REDSET_HIP_BLOCKS_PER_CU overrides it.
 int target_blocks_per_cu(int occupancy) {
   static int env = -1;
@@ -64,7 +65,7 @@ int target_blocks_per_cu(int occupancy) {
     const char* s = std::getenv("REDSET_HIP_BLOCKS_PER_CU");
     env = (s && std::atoi(s) > 0) ? std::atoi(s) : 0;
   }
-  const int want = env > 0 ? env : 2;
+  const int want = env > 0 ? env : std::max(1, 512 / redset_hip::kBlock);  // 8 waves per CU
   return std::max(1, std::min(want, occupancy));
 }
 

@@ -69,10 +69,10 @@
 
 // Register budget of the kernels: N > 0 compiles them for at most N waves
 // per SIMD (amdgpu_waves_per_eu), i.e. up to 512 / N VGPRs; 0 lets the
-// compiler aim for 4 waves (<= 128 VGPRs). The codec runs 2 blocks of 4
-// waves per CU = 2 waves per SIMD (redset_hip.cpp), so 2 costs no occupancy;
-// it lets gf_mac<8,3> issue all 8 input loads of a position before its first
-// wait and measured +1.0% on the RS step (profiles/r01_ab_waves_per_eu.txt).
+// compiler aim for 4 waves (<= 128 VGPRs). The codec runs 8 waves per CU = 2
+// per SIMD (redset_hip.cpp), so 2 costs no occupancy; it lets gf_mac<8,3>
+// issue all 8 input loads of a position before its first wait and measured
+// +1.0% on the RS step (profiles/r01_ab_waves_per_eu.txt).
 #ifndef REDSET_WAVES_PER_EU
 #define REDSET_WAVES_PER_EU 2
 #endif

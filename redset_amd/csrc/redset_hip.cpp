@@ -70,10 +70,10 @@ int target_blocks_per_cu(int occupancy) {
 }
 
 // Resident XOR blocks per CU. The XOR kernel has no tables and little VALU
-// work, so 4 waves per CU keep its 7 read streams busy with half the
-// requests in flight of the GF kernel's 8 waves: 6.00 vs 5.78 TB/s on the XOR
-// leg (profiles/r01_ab_xor_blocks.txt). REDSET_HIP_XOR_BLOCKS_PER_CU
-// overrides it (A/B).
+// work: with 256-thread blocks one block per CU (4 waves) ran its 7 read
+// streams at 6.00 TB/s against 5.78 at two (profiles/r01_ab_xor_blocks.txt);
+// with 512-thread blocks one block (8 waves) runs 5.98-6.00
+// (profiles/r01_ab_block_size.txt). REDSET_HIP_XOR_BLOCKS_PER_CU overrides it.
 int xor_blocks_cap() {
   static int env = -1;
   if (env < 0) {

@@ -409,6 +409,9 @@ def main():
             "parallelism": "single GPU" if world == 1 else f"{world} independent sets, one per GPU (no collective)",
         },
     }
+    step_ms = sorted(ev[k][0].elapsed_time(ev[k][2]) for k in range(args.steps))
+    step_ms_median = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else \
+        (step_ms[len(step_ms) // 2 - 1] + step_ms[len(step_ms) // 2]) / 2
     enc_ms = sum(ev[k][0].elapsed_time(ev[k][1]) for k in range(args.steps)) / args.steps
     reb_ms = sum(ev[k][1].elapsed_time(ev[k][2]) for k in range(args.steps)) / args.steps
     # one launch = one stripe when a plan runs its jobs one after another (the
@@ -445,6 +448,10 @@ def main():
         "encode_GBps": round(eb / (enc_ms * 1e-3) / 1e9, 1),
         "encode_read_GBps": round(enc_plan.bytes_read / (enc_ms * 1e-3) / 1e9, 1),
         "rebuild_GBps": round(rb / (reb_ms * 1e-3) / 1e9, 1),
+        # SURVEY.md §8d asks for the median of >= 10 event-timed steps beside the mean
+        "step_median_GBps": round(bytes_per_step / (step_ms_median * 1e-3) / 1e9, 1),
+        "step_event_ms": {"median": round(step_ms_median, 4), "min": round(min(step_ms), 4),
+                          "max": round(max(step_ms), 4)},
     }
     result["round_trip_bit_exact"] = rt_ok
     result["box_reference"] = {

@@ -91,6 +91,23 @@ def cpu_baseline(p, e, lost, target_s):
             break
     enc_bytes = p * (d + e) * chunk * passes
     reb_bytes = p * (d + len(lost)) * chunk * passes
+    # (ii) of SURVEY.md §8d: one thread of redset_rs_reduce_buffer_multadd's
+    # premult loop (src/redset_reedsolomon_common.c:798-811) on 64 MiB slices
+    buf = np.zeros(64 * MIB, np.uint8)
+    src = lofi[0][:64 * MIB] if lofi[0].size >= 64 * MIB else np.resize(lofi[0], 64 * MIB)
+    src = np.ascontiguousarray(src)
+    reps, t_ma = 0, 0.0
+    while t_ma < min(3.0, target_s / 3):
+        t0 = time.perf_counter()
+        st.multadd(buf, 29, src)
+        t_ma += time.perf_counter() - t0
+        reps += 1
+    cpu_model = ""
+    try:
+        with open("/proc/cpuinfo") as f:
+            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        pass
     return {
         "value": round((enc_bytes + reb_bytes) / (t_enc + t_reb) / 1e9, 4),
         "unit": "GB/s",
@@ -104,6 +121,9 @@ def cpu_baseline(p, e, lost, target_s):
         "encode_GBps": round(enc_bytes / t_enc / 1e9, 4),
         "rebuild_GBps": round(reb_bytes / t_reb / 1e9, 4),
         "host_cpus": os.cpu_count(),
+        "cpu_model": cpu_model,
+        # input bytes of one multadd (data read; the accumulator's RMW not counted), GB/s
+        "multadd_1thread_GBps": round(reps * 64 * MIB / t_ma / 1e9, 4),
     }
 
 

@@ -107,6 +107,7 @@ def _assemble(host_arrays, where, world, p, chunk, W, k, r):
 
 
 @pytest.mark.parametrize("world,p,e,chunk,lost", [(2, 4, 2, 3000, [1]), (2, 11, 3, 4096, [1, 2]), (4, 11, 3, 2048, [1, 2]),
+                                                   (8, 11, 3, 4096, [1, 2]),  # the driver's 8-GPU shape
                                                    (3, 5, 2, 1000, [0, 4])])
 def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost):
     port = _free_port()

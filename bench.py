@@ -26,6 +26,7 @@ import argparse
 import json
 import os
 import sys
+import threading
 import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -50,6 +51,8 @@ def parse():
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port beside (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
     ap.add_argument("--sharded", type=int, default=1, help="N>1: also time the RCCL sharded-rebuild leg")
+    ap.add_argument("--sharded-timeout", type=float, default=150.0,
+                    help="seconds the sharded leg may take before the main line is printed without it")
     ap.add_argument("--xor", type=int, default=1, help="also time the XOR set of configs[1] (rank 0)")
     ap.add_argument("--pairs", type=int, default=1,
                     help="also time the rebuild of every pair of erased members (rank 0; SURVEY.md §8d worst case)")
@@ -337,6 +340,32 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     return out
 
 
+_PRINT_LOCK = threading.Lock()
+_PRINTED = threading.Event()
+
+
+def emit(result, rank):
+    """Rank 0 prints the one JSON line (once, whichever thread gets here first)."""
+    with _PRINT_LOCK:
+        if rank == 0 and not _PRINTED.is_set():
+            print(json.dumps(result), flush=True)
+        _PRINTED.set()
+
+
+def sharded_expired(result, rank, limit):
+    """Watchdog of the sharded leg and the final barrier: print the line
+    measured so far if it is not out yet, then end this rank (the process
+    group is left hung, not torn down)."""
+    with _PRINT_LOCK:
+        if not _PRINTED.is_set():
+            result["sharded"] = {"error": f"timed out after {limit:g} s"}
+            if rank == 0:
+                print(json.dumps(result), flush=True)
+            _PRINTED.set()
+        print(f"rank {rank}: sharded leg or final barrier timed out after {limit:g} s", file=sys.stderr, flush=True)
+        os._exit(0)
+
+
 def main():
     args = parse()
     import torch
@@ -483,21 +512,28 @@ def main():
         result["rebuild_every_pair"] = rebuild_pairs(codec, lay, chunk, stream)
     if args.xor and rank == 0:
         result["xor"] = xor_leg(args, chunk, stream)
+    watchdog = None
     if dist_on and args.sharded:
         # second leg: the multi-rank rebuild with its RCCL exchange. It must
         # not cost the main line: a failure is reported in "sharded" (every
-        # rank runs the same collectives, so they fail alike rather than hang)
+        # rank runs the same collectives, so they fail alike). A hung exchange
+        # cannot raise: a watchdog then prints the main line with the leg
+        # marked timed out and ends every rank.
+        watchdog = threading.Timer(args.sharded_timeout, sharded_expired, (result, rank, args.sharded_timeout))
+        watchdog.daemon = True
+        watchdog.start()
         try:
             result["sharded"] = sharded_leg(args, p, e, chunk, lost, world, rank)
         except Exception as exc:  # noqa: BLE001 -- reported, not swallowed
             result["sharded"] = {"error": f"{type(exc).__name__}: {exc}"}
     if args.cpu_baseline and rank == 0 and not dist_on:
         result["cpu_baseline"] = cpu_baseline(p, e, lost, args.cpu_seconds)
-    if rank == 0:
-        print(json.dumps(result), flush=True)
+    emit(result, rank)
     if dist_on:
         dist.barrier()
         dist.destroy_process_group()
+    if watchdog is not None:
+        watchdog.cancel()
 
 
 if __name__ == "__main__":

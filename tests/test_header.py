@@ -1,0 +1,114 @@
+"""Redundancy-file headers (redset_amd/header.py) against the reference's
+documented example headers (tests/golden/header_{xor,rs}_doc.txt, made by
+tools/make_header_fixtures.py from doc/rst/schemes.rst:262-327 and :520-603).
+
+The trees are built from the examples' inputs (set of 4, member 0's header,
+the documented file stats) through the same construction as
+redset_apply_rs / redset_apply_xor (src/redset_reedsolomon.c:430-516,
+src/redset_xor.c:310-393) and must render to the documented text exactly.
+KVTree's on-disk bytes are unpinned (module docstring); the frame round trip
+and the set-facts recovery are checked on their own."""
+import os
+
+import pytest
+
+from redset_amd import header as H
+
+GOLD = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def _doc(name):
+    with open(os.path.join(GOLD, f"header_{name}_doc.txt")) as f:
+        return f.read()
+
+
+def _meta_from_doc(t, member):
+    """FileMeta inputs of the documented member (its stat values)."""
+    (path, m), = t["DESC"][str(member)]["FILE"]["0"].items()
+    g = lambda k: H.get_int(m, k)  # noqa: E731
+    return H.FileMeta(path, g("SIZE"), g("MODE"), g("UID"), g("GID"),
+                      (g("ATIME_SECS"), g("ATIME_NSECS")), (g("CTIME_SECS"), g("CTIME_NSECS")),
+                      (g("MTIME_SECS"), g("MTIME_NSECS")))
+
+
+def _build(scheme, text, encoding):
+    doc = H.parse(text)
+    p, me = 4, 0
+    members = []
+    for r in range(p):
+        if str(r) in doc["DESC"]:
+            fm = _meta_from_doc(doc, r)
+        else:  # not carried by member 0's header: any stats will do
+            fm = H.FileMeta(f"./testfile_{r}.out", 1 << 20)
+        d = H.Descriptor(scheme, r, p, r, p, encoding=encoding)
+        members.append(H.member_hash(d, [fm]))
+    max_bytes = max(H.get_int(list(m["FILE"]["0"].values())[0], "SIZE") for m in members)
+    chunk = H.chunk_size(scheme, max_bytes, p, encoding)
+    return H.header_tree(scheme, me, members, list(range(p)), chunk, encoding)
+
+
+@pytest.mark.parametrize("scheme,name,k", [("XOR", "xor", 1), ("RS", "rs", 2)])
+def test_documented_header(scheme, name, k):
+    text = _doc(name)
+    assert H.render(_build(scheme, text, k)) == text
+
+
+def test_documented_chunk_sizes():
+    # XOR example: max file 7340032 over 3 segments; RS: over 4 - 2
+    assert H.chunk_size("XOR", 7340032, 4) == 2446678
+    assert H.chunk_size("RS", 7340032, 4, 2) == 3670016
+    assert H.chunk_size("RS", 0, 4, 2) == 1          # 0-byte files, src/redset_reedsolomon.c:490-493
+    with pytest.raises(ValueError):
+        H.chunk_size("RS", 10, 3, 3)
+
+
+def test_parse_render_round_trip():
+    for name in ("xor", "rs"):
+        text = _doc(name)
+        assert H.render(H.parse(text)) == text
+
+
+def test_frame_round_trip(tmp_path):
+    t = H.parse(_doc("rs"))
+    path = str(tmp_path / "f.redset")
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    n = H.write_header(fd, t)
+    os.write(fd, b"\xAB" * 100)
+    assert os.lseek(fd, 0, os.SEEK_CUR) == n + 100
+    os.close(fd)
+    back, size = H.read_header(path)
+    assert size == n and back == t
+    with pytest.raises(ValueError):
+        H.decode(b"XXXXXXXX" + bytes(16))
+
+
+def test_filenames():
+    assert H.redundancy_filename("RS", "ckpt/", 5, 0, 2, 3, 8) == "ckpt/5.rs.grp_1_of_2.mem_4_of_8.redset"
+    assert H.redundancy_filename("XOR", "", 0, 1, 2, 0, 4) == "0.xor.grp_2_of_2.mem_1_of_4.redset"
+
+
+@pytest.mark.parametrize("scheme,p,k,lost", [("RS", 6, 2, [1, 2]), ("RS", 11, 3, [0, 9, 10]),
+                                             ("XOR", 5, 1, [4])])
+def test_set_facts_from_survivors(scheme, p, k, lost):
+    """Any k lost members' file lists come back from their right neighbours'
+    headers (each header carries its k left neighbours,
+    src/redset_reedsolomon.c:453-474)."""
+    members = []
+    for r in range(p):
+        files = [H.FileMeta(f"/d/r{r}_f{i}", 1000 * r + i) for i in range(1 + r % 3)]
+        members.append(H.member_hash(H.Descriptor(scheme, r, p, 10 + r, 64, encoding=k), files))
+    chunk = H.chunk_size(scheme, max(sum(1000 * r + i for i in range(1 + r % 3)) for r in range(p)), p, k)
+    heads = [H.decode(H.encode(H.header_tree(scheme, r, members, [10 + i for i in range(p)], chunk, k)))
+             for r in range(p) if r not in lost]
+    f = H.set_facts(heads)
+    assert (f.scheme, f.ranks, f.encoding, f.chunk) == (scheme, p, k, chunk)
+    assert f.world_ranks == [10 + i for i in range(p)]
+    assert [i for i in range(p) if not f.have_header[i]] == lost
+    for r in range(p):
+        assert f.files(r) == [(f"/d/r{r}_f{i}", 1000 * r + i) for i in range(1 + r % 3)]
+    # one more loss than k neighbours cover: some member's list is gone
+    worse = sorted(set(lost) | {(max(lost) + 1) % p} | ({(max(lost) + 2) % p} if scheme == "RS" else set()))
+    if len(worse) > k:
+        heads2 = [h for h, r in zip(heads, [r for r in range(p) if r not in lost]) if r not in worse]
+        with pytest.raises(ValueError):
+            H.set_facts(heads2)

@@ -1,0 +1,123 @@
+"""GPU tests of redundancy sets on disk with headers (redset_amd.setfiles):
+apply_set writes every member's redundancy file (header + parity), members
+are lost, and rebuild_set learns the set from the surviving headers alone
+(src/redset_reedsolomon_serial.c:355-500), rebuilds the lost members' data
+files, metadata and redundancy files, and everything must match what was
+there before byte for byte (CRC32 as test/test_redset.c:459-589 checks,
+plus the whole redundancy files, headers included). The parity bytes after
+each header are checked against the CPU oracle."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+torch = pytest.importorskip("torch")
+
+
+@pytest.fixture(scope="module")
+def sf():
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import redset_amd
+    from redset_amd import setfiles
+
+    redset_amd.load()
+    return setfiles
+
+
+def _members(tmp, p, sizes, seed):
+    rng = np.random.default_rng(seed)
+    out = []
+    for r in range(p):
+        fl = []
+        for k, size in enumerate(sizes[r]):
+            path = os.path.join(tmp, "data", f"rank{r}_file{k}.dat")
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            rng.integers(0, 256, size, dtype=np.uint8).tofile(path)
+            os.chmod(path, 0o640 if r % 2 else 0o600)
+            os.utime(path, ns=(1_596_610_023_010_398_911 + r, 1_596_610_023_005_398_943 + k))
+            fl.append(path)
+        out.append(fl)
+    return out
+
+
+def _logical(paths, total):
+    parts = [np.fromfile(p, dtype=np.uint8) for p in paths]
+    cat = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    out = np.zeros(total, np.uint8)
+    out[:cat.size] = cat
+    return out
+
+
+def _snapshot(oracle, paths):
+    snap = {}
+    for p in paths:
+        st = os.stat(p)
+        meta = (st.st_mode, st.st_mtime_ns) if not p.endswith(".redset") else ()  # data files get their stats back
+        snap[p] = (oracle.crc32(np.fromfile(p, dtype=np.uint8)), st.st_size) + meta
+    return snap
+
+
+@pytest.mark.parametrize("scheme,p,k,lost,sizes", [
+    ("XOR", 4, 1, [2], [[1 << 20]] * 4),                 # configs[0]'s shape, 1 MiB files
+    ("RS", 6, 2, [0, 4], [[300_000, 77], [1], [250_000], [0, 123_456], [199_999, 5, 60_000], [4096]]),
+    ("RS", 11, 3, [1, 2, 9], [[200_003]] * 11),
+])
+def test_apply_lose_rebuild(sf, oracle, tmp_path, scheme, p, k, lost, sizes):
+    from redset_amd import header as H
+
+    tmp = str(tmp_path)
+    members = _members(tmp, p, sizes, seed=p * 5 + k)
+    res = sf.apply_set(scheme, members, os.path.join(tmp, "ckpt."), encoding=k, slice_bytes=1 << 16)
+    reds, chunk = res["redundancy"], res["chunk"]
+    assert chunk == H.chunk_size(scheme, max(sum(os.path.getsize(f) for f in fl) for fl in members), p, k)
+    d = p - k
+    lofi = [_logical(fl, d * chunk) for fl in members]
+    want = [np.zeros(k * chunk, np.uint8) for _ in range(p)]
+    if scheme == "RS":
+        oracle.OracleRS(p, k).encode_set(lofi, want, chunk)
+    else:
+        oracle.xor_encode_set(p, lofi, want, chunk)
+    for r in range(p):
+        raw = np.fromfile(reds[r], dtype=np.uint8)
+        hs = res["header_bytes"][r]
+        assert raw.size == hs + k * chunk
+        assert np.array_equal(raw[hs:], want[r]), r
+        t, n = H.read_header(reds[r])
+        assert n == hs and H.get_int(t, "RANK") == r and H.get_int(t, "CHUNK") == chunk
+    allpaths = [f for fl in members for f in fl] + reds
+    before = _snapshot(oracle, allpaths)
+    # nothing lost: no-op
+    assert sf.rebuild_set(reds)["missing"] == []
+    for r in lost:
+        for f in members[r]:
+            os.unlink(f)
+        os.unlink(reds[r])
+    out = sf.rebuild_set(reds, slice_bytes=1 << 15)
+    assert out["missing"] == sorted(lost) and out["ok"], out
+    assert _snapshot(oracle, allpaths) == before
+
+
+def test_truncated_data_file_is_lost(sf, oracle, tmp_path):
+    tmp = str(tmp_path)
+    members = _members(tmp, 5, [[70_000, 3]] * 5, seed=9)
+    reds = sf.apply_set("RS", members, os.path.join(tmp, "c"), encoding=2)["redundancy"]
+    allpaths = [f for fl in members for f in fl] + reds
+    before = _snapshot(oracle, allpaths)
+    with open(members[3][0], "r+b") as f:
+        f.truncate(1000)
+    out = sf.rebuild_set(reds)
+    assert out["missing"] == [3] and out["ok"]
+    assert _snapshot(oracle, allpaths) == before
+
+
+def test_too_many_lost(sf, tmp_path):
+    tmp = str(tmp_path)
+    members = _members(tmp, 5, [[10_000]] * 5, seed=3)
+    reds = sf.apply_set("RS", members, os.path.join(tmp, "c"), encoding=2)["redundancy"]
+    os.unlink(members[0][0])
+    os.unlink(members[2][0])
+    os.unlink(members[4][0])
+    with pytest.raises(ValueError, match="tolerates"):
+        sf.rebuild_set(reds)

@@ -112,3 +112,39 @@ def test_set_facts_from_survivors(scheme, p, k, lost):
         heads2 = [h for h, r in zip(heads, [r for r in range(p) if r not in lost]) if r not in worse]
         with pytest.raises(ValueError):
             H.set_facts(heads2)
+
+
+def _headers_on_disk(tmp, scheme, p, k):
+    """Data files + header-only redundancy files (no parity: CPU-side checks only)."""
+    members, reds = [], []
+    for r in range(p):
+        path = os.path.join(tmp, f"r{r}.dat")
+        with open(path, "wb") as f:
+            f.write(bytes([r]) * (100 + r))
+        members.append(H.member_hash(H.Descriptor(scheme, r, p, r, p, encoding=k), [H.FileMeta.stat(path)]))
+    chunk = H.chunk_size(scheme, 100 + p - 1, p, k)
+    for r in range(p):
+        red = H.redundancy_filename(scheme, os.path.join(tmp, "ck."), r, 0, 1, r, p)
+        fd = os.open(red, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+        H.write_header(fd, H.header_tree(scheme, r, members, list(range(p)), chunk, k))
+        os.close(fd)
+        reds.append(red)
+    return reds
+
+
+def test_rebuild_set_detection_without_gpu(tmp_path):
+    """rebuild_set's set discovery and loss accounting run before any device
+    work: nothing lost is a no-op, more lost than k is refused
+    (src/redset_reedsolomon_serial.c:476-519)."""
+    from redset_amd import setfiles
+
+    tmp = str(tmp_path)
+    reds = _headers_on_disk(tmp, "RS", 6, 2)
+    out = setfiles.rebuild_set(reds)
+    assert out["missing"] == [] and out["chunk"] == H.chunk_size("RS", 105, 6, 2)
+    assert out["redundancy"] == reds
+    os.unlink(reds[1])
+    os.unlink(os.path.join(tmp, "r3.dat"))
+    os.unlink(os.path.join(tmp, "r4.dat"))
+    with pytest.raises(ValueError, match="tolerates 2"):
+        setfiles.rebuild_set(reds)

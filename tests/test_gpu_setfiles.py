@@ -121,3 +121,33 @@ def test_too_many_lost(sf, tmp_path):
     os.unlink(members[4][0])
     with pytest.raises(ValueError, match="tolerates"):
         sf.rebuild_set(reds)
+
+
+TOOL = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "redset_amd", "bin",
+                    "redset_hip_rebuild")
+
+
+@pytest.mark.parametrize("scheme,p,k,lost", [("RS", 8, 3, [0, 5, 7]), ("XOR", 4, 1, [1])])
+def test_rebuild_tool_from_headers(sf, oracle, tmp_path, scheme, p, k, lost):
+    """redset_hip_rebuild headers <files>: the C tool reads the set from the
+    surviving headers and regenerates the lost members' headers in C; the
+    whole redundancy files (headers included) and the data files with their
+    stats must come back byte for byte."""
+    import json
+    import subprocess
+
+    tmp = str(tmp_path)
+    sizes = [[150_001 + 17 * r, 3 * r] for r in range(p)]
+    members = _members(tmp, p, sizes, seed=p + k)
+    reds = sf.apply_set(scheme, members, os.path.join(tmp, "set."), encoding=k)["redundancy"]
+    allpaths = [f for fl in members for f in fl] + reds
+    before = _snapshot(oracle, allpaths)
+    for r in lost:
+        for f in members[r]:
+            os.unlink(f)
+        os.unlink(reds[r])
+    res = subprocess.run([TOOL, "headers", *reds], capture_output=True, text=True, timeout=300)
+    assert res.returncode == 0, res.stdout + res.stderr
+    out = json.loads(res.stdout)
+    assert out["missing"] == sorted(lost) and out["ok"] and out["metadata_ok"], out
+    assert _snapshot(oracle, allpaths) == before

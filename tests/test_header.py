@@ -148,3 +148,26 @@ def test_rebuild_set_detection_without_gpu(tmp_path):
     os.unlink(os.path.join(tmp, "r4.dat"))
     with pytest.raises(ValueError, match="tolerates 2"):
         setfiles.rebuild_set(reds)
+
+
+TOOL = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "redset_amd", "bin",
+                    "redset_hip_rebuild")
+
+
+@pytest.mark.skipif(not os.path.exists(TOOL), reason="redset_hip_rebuild not built")
+def test_rebuild_tool_headers_mode_without_gpu(tmp_path):
+    """The C tool's headers mode (header_tree.c) learns the same set from the
+    same headers: no-op when nothing is lost, refusal past k."""
+    import json
+    import subprocess
+
+    tmp = str(tmp_path)
+    reds = _headers_on_disk(tmp, "XOR", 5, 1)
+    res = subprocess.run([TOOL, "headers", *reds], capture_output=True, text=True, timeout=60)
+    assert res.returncode == 0, res.stderr
+    out = json.loads(res.stdout)
+    assert (out["scheme"], out["ranks"], out["encoding"], out["missing"]) == ("xor", 5, 1, [])
+    os.unlink(reds[0])
+    os.unlink(os.path.join(tmp, "r2.dat"))
+    res = subprocess.run([TOOL, "headers", *reds], capture_output=True, text=True, timeout=60)
+    assert res.returncode == 1 and "tolerates 1" in res.stderr

@@ -454,6 +454,16 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
   }
 }
 
+// Optional (A/B only): give each XCD a contiguous run of the job's block
+// windows instead of every 8th one (blocks are dealt round-robin over the
+// 8 XCDs, so blocks b and b+8 share one).
+__device__ __forceinline__ int job_block(int b, int per_job) {
+#if defined(REDSET_XCD_REMAP) && REDSET_XCD_REMAP
+  if ((per_job & 7) == 0) return (b & 7) * (per_job >> 3) + (b >> 3);
+#endif
+  return b;
+}
+
 // entry points: jobs from a device array (plans), or one job passed by
 // value in the kernel arguments (stripe primitives, no device descriptor)
 template <int NIN, int NOUT, bool ACC>
@@ -468,7 +478,7 @@ REDSET_KERNEL gf_mac_kernel(GfLaunch L) {
     return;
   }
   const int job = blockIdx.x / L.blocks_per_job;
-  gf_mac_body<NIN, NOUT, ACC>(L, L.jobs[L.job0 + job], blockIdx.x - job * L.blocks_per_job);
+  gf_mac_body<NIN, NOUT, ACC>(L, L.jobs[L.job0 + job], job_block(blockIdx.x - job * L.blocks_per_job, L.blocks_per_job));
 }
 
 template <int NIN, int NOUT, bool ACC>
@@ -483,7 +493,7 @@ REDSET_KERNEL xor_kernel(XorLaunch L) {
     return;
   }
   const int job = blockIdx.x / L.blocks_per_job;
-  xor_body<NIN, ACC>(L, L.jobs[L.job0 + job], blockIdx.x - job * L.blocks_per_job);
+  xor_body<NIN, ACC>(L, L.jobs[L.job0 + job], job_block(blockIdx.x - job * L.blocks_per_job, L.blocks_per_job));
 }
 
 template <int NIN, bool ACC>

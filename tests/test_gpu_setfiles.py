@@ -151,3 +151,35 @@ def test_rebuild_tool_from_headers(sf, oracle, tmp_path, scheme, p, k, lost):
     out = json.loads(res.stdout)
     assert out["missing"] == sorted(lost) and out["ok"] and out["metadata_ok"], out
     assert _snapshot(oracle, allpaths) == before
+
+
+@pytest.mark.parametrize("use_tool", [False, True])
+def test_rebuild_in_a_strided_group(sf, oracle, tmp_path, use_tool):
+    """Set members at parent ranks 3, 7, 11, ... in group 2 of 4: the lost
+    members' redundancy file names come back from the GROUP map and the
+    descriptors (rs.grp_2_of_4.mem_<r+1>_of_6, src/redset_reedsolomon.c:34-44)."""
+    import json
+    import subprocess
+
+    tmp = str(tmp_path)
+    p, k, lost = 6, 2, [2, 3]
+    members = _members(tmp, p, [[40_000 + r] for r in range(p)], seed=21)
+    world = [3 + 4 * r for r in range(p)]
+    res = sf.apply_set("RS", members, os.path.join(tmp, "g."), encoding=k, world_ranks=world, world_size=32,
+                       group_id=1, groups=4)
+    reds = res["redundancy"]
+    assert os.path.basename(reds[2]) == "g.11.rs.grp_2_of_4.mem_3_of_6.redset"
+    allpaths = [f for fl in members for f in fl] + reds
+    before = _snapshot(oracle, allpaths)
+    for r in lost:
+        os.unlink(members[r][0])
+        os.unlink(reds[r])
+    survivors = [x for i, x in enumerate(reds) if i not in lost]
+    if use_tool:
+        out = subprocess.run([TOOL, "headers", *survivors], capture_output=True, text=True, timeout=300)
+        assert out.returncode == 0, out.stdout + out.stderr
+        assert json.loads(out.stdout)["missing"] == lost
+    else:
+        out = sf.rebuild_set(survivors)
+        assert out["missing"] == lost and out["redundancy"] == reds and out["ok"]
+    assert _snapshot(oracle, allpaths) == before

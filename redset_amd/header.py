@@ -234,6 +234,8 @@ def member_hash(desc: Descriptor, files: Sequence[FileMeta]) -> Tree:
     set_kv(t, "FILES", len(files))
     ft: Tree = {}
     for i, fm in enumerate(files):
+        if " = " in fm.path or "\n" in fm.path or fm.path != fm.path.strip(" ") or not fm.path:
+            raise ValueError(f"file name {fm.path!r} has no representation in the header text form")
         ft[str(i)] = {fm.path: fm.tree()}
     t["FILE"] = ft
     t["DESC"] = desc.tree()

@@ -171,3 +171,12 @@ def test_rebuild_tool_headers_mode_without_gpu(tmp_path):
     os.unlink(os.path.join(tmp, "r2.dat"))
     res = subprocess.run([TOOL, "headers", *reds], capture_output=True, text=True, timeout=60)
     assert res.returncode == 1 and "tolerates 1" in res.stderr
+
+
+def test_unrepresentable_file_names():
+    d = H.Descriptor("RS", 0, 4, 0, 4, encoding=2)
+    for bad in ("a = b", "x\ny", " lead", ""):
+        with pytest.raises(ValueError):
+            H.member_hash(d, [H.FileMeta(bad, 1)])
+    t = H.member_hash(d, [H.FileMeta("/dir with space/f.dat", 7)])
+    assert H.parse(H.render(t)) == t

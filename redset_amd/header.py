@@ -103,7 +103,7 @@ def parse(text: str) -> Tree:
     """Inverse of :func:`render` (keys must not contain " = ")."""
     root: Tree = {}
     stack: List[Tuple[int, Tree]] = [(-1, root)]
-    for n, line in enumerate(text.splitlines(), 1):
+    for line in text.splitlines():
         if not line.strip():
             continue
         ind = len(line) - len(line.lstrip(" "))

@@ -35,6 +35,7 @@
  *
  * usage: redset_hip_rebuild rs|xor <ranks> <encoding> <dir>
  *        redset_hip_rebuild headers <redundancy file>...
+ *        redset_hip_rebuild print-header <redundancy file>   (header text form)
  * Prints one JSON line with what was rebuilt and the stream statistics.
  */
 #include <errno.h>
@@ -236,6 +237,21 @@ static int apply_meta(const char* path, const htree* meta) {
 }
 
 int main(int argc, char** argv) {
+  if (argc == 3 && strcmp(argv[1], "print-header") == 0) {
+    int fd = open(argv[2], O_RDONLY);
+    unsigned long long hs = 0;
+    htree* h = fd < 0 ? NULL : ht_read_header(fd, &hs);
+    if (fd >= 0) close(fd);
+    if (!h) {
+      fprintf(stderr, "redset_hip_rebuild: %s: no readable header\n", argv[2]);
+      return 1;
+    }
+    char* text = ht_render(h);
+    fputs(text, stdout);
+    free(text);
+    ht_free(h);
+    return 0;
+  }
   const int hdr_mode = argc >= 3 && strcmp(argv[1], "headers") == 0;
   if (!hdr_mode && (argc != 5 || (strcmp(argv[1], "rs") != 0 && strcmp(argv[1], "xor") != 0))) {
     fprintf(stderr, "usage: %s rs|xor <ranks> <encoding> <dir>\n       %s headers <redundancy file>...\n", argv[0],

@@ -180,3 +180,20 @@ def test_unrepresentable_file_names():
             H.member_hash(d, [H.FileMeta(bad, 1)])
     t = H.member_hash(d, [H.FileMeta("/dir with space/f.dat", 7)])
     assert H.parse(H.render(t)) == t
+
+
+@pytest.mark.skipif(not os.path.exists(TOOL), reason="redset_hip_rebuild not built")
+@pytest.mark.parametrize("name", ["xor", "rs"])
+def test_c_header_reader_renders_documented_header(tmp_path, name):
+    """header_tree.c parses the framed header and renders the reference's
+    documented text byte for byte (the C twin of test_documented_header)."""
+    import subprocess
+
+    text = _doc(name)
+    path = str(tmp_path / "h.redset")
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    H.write_header(fd, H.parse(text))
+    os.close(fd)
+    res = subprocess.run([TOOL, "print-header", path], capture_output=True, text=True, timeout=60)
+    assert res.returncode == 0, res.stderr
+    assert res.stdout == text

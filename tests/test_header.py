@@ -197,3 +197,22 @@ def test_c_header_reader_renders_documented_header(tmp_path, name):
     res = subprocess.run([TOOL, "print-header", path], capture_output=True, text=True, timeout=60)
     assert res.returncode == 0, res.stderr
     assert res.stdout == text
+
+
+def test_corrupt_headers_count_as_lost(tmp_path):
+    """A redundancy file whose header cannot be read is a lost member, in
+    the Python rebuild and in the C tool alike (src/redset_reedsolomon_serial.c:370-382)."""
+    import subprocess
+
+    from redset_amd import setfiles
+
+    tmp = str(tmp_path)
+    reds = _headers_on_disk(tmp, "XOR", 5, 1)
+    for r in (1, 3):
+        with open(reds[r], "r+b") as f:
+            f.write(b"garbage!")
+    with pytest.raises(ValueError, match="tolerates 1"):
+        setfiles.rebuild_set(reds)
+    if os.path.exists(TOOL):
+        res = subprocess.run([TOOL, "headers", *reds], capture_output=True, text=True, timeout=60)
+        assert res.returncode == 1 and "2 members missing" in res.stderr, res.stderr

@@ -55,6 +55,54 @@ __global__ void __launch_bounds__(B) w_streams(uint4* __restrict__ b, size_t n) 
   }
 }
 
+// S streams, each written by its own third of the grid (block b -> stream
+// b % S): same fronts, each 1/S as wide as in w_streams
+template <int S, int B>
+__global__ void __launch_bounds__(B) w_split(uint4* __restrict__ b, size_t n) {
+  const size_t m = n / S;
+  const int s = blockIdx.x % S, nb = gridDim.x / S;
+  const size_t stride = (size_t)nb * B;
+  for (size_t base = (size_t)(blockIdx.x / S) * B + threadIdx.x; base < m; base += stride)
+    b[(size_t)s * m + base] = make_uint4((uint32_t)base, s, 1, 2);
+}
+
+// S streams one after another (one front at a time), same grid
+template <int S, int B>
+__global__ void __launch_bounds__(B) w_seq(uint4* __restrict__ b, size_t n) {
+  const size_t m = n / S;
+  const size_t stride = (size_t)gridDim.x * B;
+  for (int s = 0; s < S; ++s)
+    for (size_t base = (size_t)blockIdx.x * B + threadIdx.x; base < m; base += stride)
+      b[(size_t)s * m + base] = make_uint4((uint32_t)base, s, 1, 2);
+}
+
+// R reads + W writes per position like rw_streams, but each half of a
+// 512-thread block sweeps its own half of the regions: two fronts per
+// stream, each G*256*16 B wide (HALVES=1: one front G*512*16 B wide)
+template <int R, int W, int HALVES>
+__global__ void __launch_bounds__(512) rw_halves(uint4* __restrict__ b, size_t n) {
+  const size_t m = n / (R + W);
+  const int h = HALVES ? threadIdx.x / 256 : 0;
+  const int t = HALVES ? threadIdx.x % 256 : threadIdx.x;
+  const int BW = HALVES ? 256 : 512;
+  const size_t lo = HALVES ? (h ? m / 2 : 0) : 0, hi = HALVES ? (h ? m : m / 2) : m;
+  const size_t stride = (size_t)gridDim.x * BW;
+  for (size_t base = lo + (size_t)blockIdx.x * BW + t; base < hi; base += stride) {
+    uint4 acc = make_uint4(0, 0, 0, 0);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      uint4 v = b[(size_t)r * m + base];
+      acc.x ^= v.x; acc.y ^= v.y; acc.z ^= v.z; acc.w ^= v.w;
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      uint4 v = acc;
+      v.x += w;
+      b[(size_t)(R + w) * m + base] = v;
+    }
+  }
+}
+
 // the encode's memory pattern without the GF math: R input streams read,
 // combined by XOR, W output streams written, each stream its own region
 template <int R, int W, int U, int B>
@@ -118,34 +166,20 @@ int main() {
   CHECK(hipMalloc(&buf, bytes));
   CHECK(hipMemset(buf, 0, bytes));
   const int reps = 10;
-  // streams side by side at the smallest write front
-  for (int g : {128, 256, 512}) {
-    RUN("streams1 U=1 B=256", (w_streams<1, 1, 256>), g, 256)
-    RUN("streams2 U=1 B=256", (w_streams<2, 1, 256>), g, 256)
-    RUN("streams3 U=1 B=256", (w_streams<3, 1, 256>), g, 256)
-  }
-  // 8 reads + 3 writes (encode) and 8 + 2 (rebuild): GB/s = (R+W) streams' bytes
-  printf("-- read/write mix (bytes = all streams)\n");
-  for (int g : {256, 512, 1024, 2048}) {
-    RUN("r8w3 U=1 B=256", (rw_streams<8, 3, 1, 256>), g, 256)
-    RUN("r8w3 U=1 B=512", (rw_streams<8, 3, 1, 512>), g, 512)
-    RUN("r8w3 U=2 B=256", (rw_streams<8, 3, 2, 256>), g, 256)
-    RUN("r8w3 U=2 B=512", (rw_streams<8, 3, 2, 512>), g, 512)
-    RUN("r8w2 U=1 B=512", (rw_streams<8, 2, 1, 512>), g, 512)
-    RUN("r8w2 U=2 B=256", (rw_streams<8, 2, 2, 256>), g, 256)
-  }
-  for (int round = 0; round < 1; ++round) {
-    printf("-- round %d (write-only GB/s)\n", round);
-    for (int g : {256, 512, 1024, 2048, 4096}) {
-      RUN("gs U=1 B=256", (w_gs<1, 256>), g, 256)
-      RUN("gs U=4 B=256", (w_gs<4, 256>), g, 256)
-      RUN("gs U=8 B=256", (w_gs<8, 256>), g, 256)
-      RUN("gs U=2 B=512", (w_gs<2, 512>), g, 512)
-      RUN("gs U=4 B=1024", (w_gs<4, 1024>), g, 1024)
-      RUN("blk U=4 B=256", (w_blk<4, 256>), g, 256)
-      RUN("streams3 U=1 B=512", (w_streams<3, 1, 512>), g, 512)
-      RUN("streams3 U=2 B=512", (w_streams<3, 2, 512>), g, 512)
-    }
+  // regions aligned: n divisible by (R+W) * 1 MiB / 16 is not needed for the
+  // write-only shapes (m = n); rw shapes use m = n / 11 as before
+  for (int round = 0; round < 2; ++round) {
+    printf("-- round %d: window width (write-only, one stream)\n", round);
+    RUN("w B=256 G=256 (1MiB)", (w_gs<1, 256>), 256, 256)
+    RUN("w B=512 G=256 (2MiB)", (w_gs<1, 512>), 256, 512)
+    RUN("w B=512 G=128 (1MiB)", (w_gs<1, 512>), 128, 512)
+    RUN("w B=1024 G=128 (2MiB)", (w_gs<1, 1024>), 128, 1024)
+    printf("-- round %d: r8w3 / r8w2, one 2 MiB front vs two 1 MiB fronts per stream (512-thread blocks)\n", round);
+    RUN("r8w3 one front G=256", (rw_halves<8, 3, 0>), 256, 512)
+    RUN("r8w3 two fronts G=256", (rw_halves<8, 3, 1>), 256, 512)
+    RUN("r8w2 one front G=256", (rw_halves<8, 2, 0>), 256, 512)
+    RUN("r8w2 two fronts G=256", (rw_halves<8, 2, 1>), 256, 512)
+    RUN("r8w3 one front G=128", (rw_halves<8, 3, 0>), 128, 512)
   }
   CHECK(hipFree(buf));
   return 0;

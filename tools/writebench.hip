@@ -103,6 +103,51 @@ __global__ void __launch_bounds__(512) rw_halves(uint4* __restrict__ b, size_t n
   }
 }
 
+// split roles: waves 0-3 of a 512-thread block only load (R streams, U
+// positions per iteration) and XOR into an LDS ring; waves 4-7 only store
+// the W outputs of the previous iteration (one wave per SIMD writing)
+template <int R, int W, int U>
+__global__ void __launch_bounds__(512) rw_roles(uint4* __restrict__ b, size_t n) {
+  __shared__ uint4 ring[2][U][256];
+  const size_t m = n / (R + W);
+  const bool loader = threadIdx.x < 256;
+  const int t = threadIdx.x & 255;
+  const size_t stride = (size_t)gridDim.x * 256 * U;
+  const size_t first = (size_t)blockIdx.x * 256 * U;
+  const long iters = first < m ? (long)((m - first + stride - 1) / stride) : 0;
+  for (long it = 0; it <= iters; ++it) {
+    if (loader && it < iters) {
+      const size_t base = first + (size_t)it * stride + t;
+      uint4 acc[U];
+#pragma unroll
+      for (int u = 0; u < U; ++u) acc[u] = make_uint4(0, 0, 0, 0);
+#pragma unroll
+      for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (base + (size_t)u * 256 < m) {
+            uint4 v = b[(size_t)r * m + base + (size_t)u * 256];
+            acc[u].x ^= v.x; acc[u].y ^= v.y; acc[u].z ^= v.z; acc[u].w ^= v.w;
+          }
+#pragma unroll
+      for (int u = 0; u < U; ++u) ring[it & 1][u][t] = acc[u];
+    }
+    if (!loader && it > 0) {
+      const size_t base = first + (size_t)(it - 1) * stride + t;
+#pragma unroll
+      for (int w = 0; w < W; ++w)
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+          if (base + (size_t)u * 256 < m) {
+            uint4 v = ring[(it - 1) & 1][u][t];
+            v.x += w;
+            b[(size_t)(R + w) * m + base + (size_t)u * 256] = v;
+          }
+    }
+    __syncthreads();
+  }
+}
+
 // the encode's memory pattern without the GF math: R input streams read,
 // combined by XOR, W output streams written, each stream its own region
 template <int R, int W, int U, int B>
@@ -166,20 +211,15 @@ int main() {
   CHECK(hipMalloc(&buf, bytes));
   CHECK(hipMemset(buf, 0, bytes));
   const int reps = 10;
-  // regions aligned: n divisible by (R+W) * 1 MiB / 16 is not needed for the
-  // write-only shapes (m = n); rw shapes use m = n / 11 as before
-  for (int round = 0; round < 2; ++round) {
-    printf("-- round %d: window width (write-only, one stream)\n", round);
-    RUN("w B=256 G=256 (1MiB)", (w_gs<1, 256>), 256, 256)
-    RUN("w B=512 G=256 (2MiB)", (w_gs<1, 512>), 256, 512)
-    RUN("w B=512 G=128 (1MiB)", (w_gs<1, 512>), 128, 512)
-    RUN("w B=1024 G=128 (2MiB)", (w_gs<1, 1024>), 128, 1024)
-    printf("-- round %d: r8w3 / r8w2, one 2 MiB front vs two 1 MiB fronts per stream (512-thread blocks)\n", round);
+  for (int round = 0; round < 3; ++round) {
+    printf("-- round %d: split roles (4 load waves + 4 store waves per 512-thread block) vs one front\n", round);
     RUN("r8w3 one front G=256", (rw_halves<8, 3, 0>), 256, 512)
-    RUN("r8w3 two fronts G=256", (rw_halves<8, 3, 1>), 256, 512)
+    RUN("r8w3 roles U=1 G=256", (rw_roles<8, 3, 1>), 256, 512)
+    RUN("r8w3 roles U=2 G=256", (rw_roles<8, 3, 2>), 256, 512)
+    RUN("r8w3 roles U=4 G=256", (rw_roles<8, 3, 4>), 256, 512)
+    RUN("r8w3 roles U=2 G=512", (rw_roles<8, 3, 2>), 512, 512)
     RUN("r8w2 one front G=256", (rw_halves<8, 2, 0>), 256, 512)
-    RUN("r8w2 two fronts G=256", (rw_halves<8, 2, 1>), 256, 512)
-    RUN("r8w3 one front G=128", (rw_halves<8, 3, 0>), 128, 512)
+    RUN("r8w2 roles U=2 G=256", (rw_roles<8, 2, 2>), 256, 512)
   }
   CHECK(hipFree(buf));
   return 0;

@@ -267,7 +267,8 @@ int main(int argc, char** argv) {
     if (load_headers(argc - 2, argv + 2, &ranks, &rs_scheme, &encoding, &m, &group) != 0) return 1;
     missing = calloc((size_t) ranks, sizeof(int));
     for (int r = 0; r < ranks; ++r) {
-      int gone = m[r].header == 0;
+      /* no readable header, parity cut short, or a data file absent / resized */
+      int gone = m[r].header == 0 || !file_ok(m[r].red, m[r].header + (unsigned long long) encoding * m[r].chunk);
       for (int k = 0; k < m[r].nfiles; ++k) gone |= !exact_size(m[r].paths[k], m[r].sizes[k]);
       if (gone) missing[nmissing++] = r;
     }

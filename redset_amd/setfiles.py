@@ -103,9 +103,10 @@ def _apply_meta(path: str, meta: H.Tree) -> List[str]:
 def rebuild_set(redundancy_files: Sequence[str], slice_bytes: int = 0) -> Dict:
     """Rebuild the lost members of one set from the redundancy files that can
     still be read (``redundancy_files`` may name lost ones too). A member is
-    lost when its redundancy file is unreadable or one of its data files is
-    absent or the wrong size. More lost members than the scheme tolerates is
-    an error (src/redset_reedsolomon_serial.c:496-519). Lost members get
+    lost when its redundancy file is unreadable or shorter than header + k
+    chunks, or one of its data files is absent or the wrong size. More lost
+    members than the scheme tolerates is an error
+    (src/redset_reedsolomon_serial.c:496-519). Lost members get
     their data files, file metadata and redundancy file (header regenerated
     from the set facts, so it matches what apply_set wrote) back."""
     heads, paths = [], {}
@@ -129,7 +130,14 @@ def rebuild_set(redundancy_files: Sequence[str], slice_bytes: int = 0) -> Dict:
     reds = [paths.get(r) or H.redundancy_filename(f.scheme, prefix, f.world_ranks[r], g, gs, r, p)
             for r in range(p)]
     files = [f.files(r) for r in range(p)]
-    lost = [r for r in range(p) if not f.have_header[r] or not _files_ok(files[r])]
+
+    def parity_ok(r: int) -> bool:  # header + k chunks present
+        try:
+            return os.stat(reds[r]).st_size >= f.header_size[r] + k * f.chunk
+        except OSError:
+            return False
+
+    lost = [r for r in range(p) if not f.have_header[r] or not parity_ok(r) or not _files_ok(files[r])]
     out = {"scheme": f.scheme, "ranks": p, "encoding": k, "chunk": f.chunk, "missing": lost,
            "redundancy": reds, "errors": []}
     if not lost:

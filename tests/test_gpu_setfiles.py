@@ -183,3 +183,23 @@ def test_rebuild_in_a_strided_group(sf, oracle, tmp_path, use_tool):
         out = sf.rebuild_set(survivors)
         assert out["missing"] == lost and out["redundancy"] == reds and out["ok"]
     assert _snapshot(oracle, allpaths) == before
+
+
+@pytest.mark.parametrize("use_tool", [False, True])
+def test_truncated_parity_is_lost(sf, oracle, tmp_path, use_tool):
+    """A redundancy file cut short after its header is a lost member too."""
+    import subprocess
+
+    tmp = str(tmp_path)
+    members = _members(tmp, 5, [[30_000]] * 5, seed=13)
+    reds = sf.apply_set("RS", members, os.path.join(tmp, "t"), encoding=2)["redundancy"]
+    allpaths = [f for fl in members for f in fl] + reds
+    before = _snapshot(oracle, allpaths)
+    with open(reds[4], "r+b") as f:
+        f.truncate(os.path.getsize(reds[4]) - 1)
+    if use_tool:
+        res = subprocess.run([TOOL, "headers", *reds], capture_output=True, text=True, timeout=300)
+        assert res.returncode == 0, res.stdout + res.stderr
+    else:
+        assert sf.rebuild_set(reds)["missing"] == [4]
+    assert _snapshot(oracle, allpaths) == before

@@ -115,7 +115,7 @@ def test_set_facts_from_survivors(scheme, p, k, lost):
 
 
 def _headers_on_disk(tmp, scheme, p, k):
-    """Data files + header-only redundancy files (no parity: CPU-side checks only)."""
+    """Data files + redundancy files with zero parity (CPU-side checks only)."""
     members, reds = [], []
     for r in range(p):
         path = os.path.join(tmp, f"r{r}.dat")
@@ -127,6 +127,7 @@ def _headers_on_disk(tmp, scheme, p, k):
         red = H.redundancy_filename(scheme, os.path.join(tmp, "ck."), r, 0, 1, r, p)
         fd = os.open(red, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
         H.write_header(fd, H.header_tree(scheme, r, members, list(range(p)), chunk, k))
+        os.write(fd, bytes(k * chunk))  # parity-sized payload (contents unused here)
         os.close(fd)
         reds.append(red)
     return reds

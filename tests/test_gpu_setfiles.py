@@ -127,7 +127,7 @@ TOOL = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
                     "redset_hip_rebuild")
 
 
-@pytest.mark.parametrize("scheme,p,k,lost", [("RS", 8, 3, [0, 5, 7]), ("XOR", 4, 1, [1])])
+@pytest.mark.parametrize("scheme,p,k,lost", [("RS", 8, 3, [0, 5, 7]), ("RS", 11, 3, [0, 9, 10]), ("XOR", 4, 1, [1])])
 def test_rebuild_tool_from_headers(sf, oracle, tmp_path, scheme, p, k, lost):
     """redset_hip_rebuild headers <files>: the C tool reads the set from the
     surviving headers and regenerates the lost members' headers in C; the

@@ -217,3 +217,23 @@ def test_corrupt_headers_count_as_lost(tmp_path):
     if os.path.exists(TOOL):
         res = subprocess.run([TOOL, "headers", *reds], capture_output=True, text=True, timeout=60)
         assert res.returncode == 1 and "2 members missing" in res.stderr, res.stderr
+
+
+@pytest.mark.skipif(not os.path.exists(TOOL), reason="redset_hip_rebuild not built")
+def test_c_and_python_agree_on_multi_digit_order(tmp_path):
+    """Members 0, 9, 10 of an 11-member set under DESC, GROUP RANK 0..10:
+    both renderers sort keys as byte strings ("10" before "9")."""
+    import subprocess
+
+    p, k = 11, 3
+    members = [H.member_hash(H.Descriptor("RS", r, p, 100 + r, 128, encoding=k),
+                             [H.FileMeta(f"/ckpt/rank{r}.dat", 1000 + r)]) for r in range(p)]
+    t = H.header_tree("RS", 0, members, [100 + r for r in range(p)], H.chunk_size("RS", 1010, p, k), k)
+    text = H.render(t)
+    assert text.index("\n  10\n") < text.index("\n  9\n")
+    path = str(tmp_path / "h.redset")
+    fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+    H.write_header(fd, t)
+    os.close(fd)
+    res = subprocess.run([TOOL, "print-header", path], capture_output=True, text=True, timeout=60)
+    assert res.returncode == 0 and res.stdout == text

@@ -128,7 +128,10 @@ int hip_ok(hipError_t e, const char* what) { return e == hipSuccess ? 0 : fail("
 int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice, int io_threads,
                  const redset_hip_io* io, redset_hip_stream_stats* stats) {
   if (!io || !io->read || !io->write) return fail("null redset_hip_io");
-  if (slice == 0) slice = 8u << 20;
+  // default slice: 8 MiB; a chunk that would fit one slice is cut into ~16
+  // slices of >= 256 KiB instead, so small sets pipeline and pin less
+  // (configs[0]'s 5.6 MB chunks: apply 58 -> 29 ms, profiles/r01_config1_headers_e2e.jsonl)
+  if (slice == 0) slice = chunk > (8u << 20) ? (8u << 20) : std::max<size_t>(256u << 10, chunk / 16);
   slice = std::min(slice, std::max<size_t>(chunk, 1));
   slice = (slice + 255) & ~static_cast<size_t>(255);
   if (io_threads <= 0) io_threads = 8;

@@ -4,7 +4,7 @@ headers + parity; member 2 is lost; rebuild_set (Python) and
 redset_hip_rebuild headers (C) rebuild it from the surviving headers.
 Files live in a tmpfs directory so the numbers are the pipeline's, not a
 disk's. Prints one JSON line per phase.
-usage: python tools/config1_e2e.py [dir] [reps]"""
+usage: python tools/config1_e2e.py [dir] [reps] [slice_bytes]"""
 import json
 import os
 import shutil
@@ -32,6 +32,7 @@ def crc(path):
 def main():
     base = sys.argv[1] if len(sys.argv) > 1 else "/dev/shm"
     reps = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+    sb = int(sys.argv[3]) if len(sys.argv) > 3 else 0
     tmp = tempfile.mkdtemp(prefix="redset_c1_", dir=base)
     try:
         p, size, lost = 4, 16 << 20, 2
@@ -46,12 +47,12 @@ def main():
         t = []
         for _ in range(reps):
             t0 = time.perf_counter()
-            res = setfiles.apply_set("XOR", files, os.path.join(tmp, "ckpt."))
+            res = setfiles.apply_set("XOR", files, os.path.join(tmp, "ckpt."), slice_bytes=sb)
             t.append(time.perf_counter() - t0)
         reds = res["redundancy"]
         chunk = res["chunk"]
         algo = p * (p - 1) * chunk + p * chunk  # read every member's 3 segments, write 4 parity cells
-        print(json.dumps({"phase": "apply_set", "chunk": chunk, "median_s": float(np.median(t)),
+        print(json.dumps({"phase": "apply_set", "chunk": chunk, "slice_bytes": sb, "median_s": float(np.median(t)),
                           "GBps": algo / float(np.median(t)) / 1e9, "reps": reps}), flush=True)
         for mode in ("rebuild_set", "tool_headers"):
             t = []
@@ -60,7 +61,7 @@ def main():
                 os.unlink(reds[lost])
                 t0 = time.perf_counter()
                 if mode == "rebuild_set":
-                    out = setfiles.rebuild_set(reds)
+                    out = setfiles.rebuild_set(reds, slice_bytes=sb)
                     ok = out["ok"] and out["missing"] == [lost]
                 else:
                     r = subprocess.run([TOOL, "headers", *reds], capture_output=True, text=True, timeout=120)
@@ -70,7 +71,7 @@ def main():
                 assert all(crc(f) == c for f, c in want.items()), mode
             # survivors' files and parity in, the lost file and its parity out: 16 C
             algo = (p - 1) * (p - 1) * chunk + (p - 1) * chunk + (p - 1) * chunk + chunk
-            print(json.dumps({"phase": mode, "median_s": float(np.median(t)), "GBps": algo / float(np.median(t)) / 1e9,
+            print(json.dumps({"phase": mode, "slice_bytes": sb, "median_s": float(np.median(t)), "GBps": algo / float(np.median(t)) / 1e9,
                               "reps": reps, "crc_ok": True}), flush=True)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)

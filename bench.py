@@ -47,9 +47,12 @@ def parse():
     ap.add_argument("--lost", default="1,2", help="members rebuilt each step")
     ap.add_argument("--cell-pad-mib", type=float, default=16.0,
                     help="MiB of padding after every cell in HBM: breaks the 2^26-byte aliasing of 64 MiB "
-                         "cells (+1-10%% depending on the box, profiles/r01_cell_placement.txt)")
+                         "cells (+2.0%% with stripes in sequence over three alternating pairs, "
+                         "profiles/r02_ab_cell_pad.txt; +1-10%% before, profiles/r01_cell_placement.txt)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port beside (rank 0, N=1)")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration (RS; XOR gets half)")
+    ap.add_argument("--cpu-chunk-mib", type=float, default=0.0,
+                    help="chunk of the CPU baseline's set (0: the GPU workload's own chunk)")
     ap.add_argument("--sharded", type=int, default=1, help="N>1: also time the RCCL sharded-rebuild leg")
     ap.add_argument("--sharded-timeout", type=float, default=150.0,
                     help="seconds the sharded leg may take before the main line is printed without it")
@@ -62,12 +65,27 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(p, e, lost, target_s):
+def _host_random(n, rng):
+    import numpy as np
+
+    return np.frombuffer(bytearray(rng.bytes(n)), dtype=np.uint8)
+
+
+def _cpu_model():
+    try:
+        with open("/proc/cpuinfo") as f:
+            return next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
+    except OSError:
+        return ""
+
+
+def cpu_baseline(p, e, lost, target_s, chunk):
     """Reference CPU path on host cores: redset_reedsolomon_encode_pthreads
     (src/redset_reedsolomon_pthreads.c:567-699) for the encode and the serial
     CPU decode the reference falls back to for PTHREADS (src/redset_reedsolomon.c:
-    994-1000), both as restated in oracle/ (kind "port"), on a bounded sample:
-    the same set shape with a smaller chunk."""
+    994-1000), both as restated in oracle/ (kind "port"), on the bench's own
+    set shape and chunk size (64 MiB cells by default: 5.6 GiB of data in
+    host memory); passes repeat until `target_s` of CPU work is done."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import numpy as np
     import oracle_lib
@@ -75,8 +93,9 @@ def cpu_baseline(p, e, lost, target_s):
     oracle_lib.build()
     st = oracle_lib.OracleRS(p, e)
     d = p - e
-    chunk = 4 * MIB
-    lofi, parity = oracle_lib.random_set(p, d, e, chunk, seed=7)
+    rng = np.random.default_rng(7)
+    lofi = [_host_random(d * chunk, rng) for _ in range(p)]
+    parity = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     passes, t_enc, t_reb, threads = 0, 0.0, 0.0, 0
     t_start = time.perf_counter()
     while True:
@@ -84,7 +103,7 @@ def cpu_baseline(p, e, lost, target_s):
         threads = st.encode_pthreads(lofi, parity, chunk, slice_bytes=MIB)
         t1 = time.perf_counter()
         lf = [x if r not in lost else np.zeros_like(x) for r, x in enumerate(lofi)]
-        pr = [x.copy() if r not in lost else np.zeros_like(x) for r, x in enumerate(parity)]
+        pr = [x if r not in lost else np.zeros_like(x) for r, x in enumerate(parity)]
         st.rebuild_set(lost, lf, pr, chunk, slice_bytes=MIB)
         t2 = time.perf_counter()
         t_enc += t1 - t0
@@ -92,25 +111,19 @@ def cpu_baseline(p, e, lost, target_s):
         passes += 1
         if time.perf_counter() - t_start >= target_s:
             break
+    ok = all(np.array_equal(lf[r], lofi[r]) and np.array_equal(pr[r], parity[r]) for r in lost)
     enc_bytes = p * (d + e) * chunk * passes
     reb_bytes = p * (d + len(lost)) * chunk * passes
     # (ii) of SURVEY.md §8d: one thread of redset_rs_reduce_buffer_multadd's
     # premult loop (src/redset_reedsolomon_common.c:798-811) on 64 MiB slices
     buf = np.zeros(64 * MIB, np.uint8)
-    src = lofi[0][:64 * MIB] if lofi[0].size >= 64 * MIB else np.resize(lofi[0], 64 * MIB)
-    src = np.ascontiguousarray(src)
+    src = np.ascontiguousarray(lofi[0][:64 * MIB])
     reps, t_ma = 0, 0.0
     while t_ma < min(3.0, target_s / 3):
         t0 = time.perf_counter()
         st.multadd(buf, 29, src)
         t_ma += time.perf_counter() - t0
         reps += 1
-    cpu_model = ""
-    try:
-        with open("/proc/cpuinfo") as f:
-            cpu_model = next((ln.split(":", 1)[1].strip() for ln in f if ln.startswith("model name")), "")
-    except OSError:
-        pass
     return {
         "value": round((enc_bytes + reb_bytes) / (t_enc + t_reb) / 1e9, 4),
         "unit": "GB/s",
@@ -118,15 +131,60 @@ def cpu_baseline(p, e, lost, target_s):
         "kind": "port",
         "sample": (
             f"{passes} x (RS({d}+{e}) full-set encode with {threads} pthreads + serial rebuild of "
-            f"members {lost}), p={p}, chunk={chunk // MIB} MiB (host buffers); encode "
+            f"members {lost}), p={p}, chunk={chunk / MIB:g} MiB (host buffers, the GPU workload's shape); encode "
             f"{enc_bytes / t_enc / 1e9:.3f} GB/s, rebuild {reb_bytes / t_reb / 1e9:.3f} GB/s"
         ),
         "encode_GBps": round(enc_bytes / t_enc / 1e9, 4),
         "rebuild_GBps": round(reb_bytes / t_reb / 1e9, 4),
+        "round_trip_equal": ok,
         "host_cpus": os.cpu_count(),
-        "cpu_model": cpu_model,
+        "cpu_model": _cpu_model(),
         # input bytes of one multadd (data read; the accumulator's RMW not counted), GB/s
         "multadd_1thread_GBps": round(reps * 64 * MIB / t_ma / 1e9, 4),
+    }
+
+
+def cpu_baseline_xor(p, root, target_s, chunk):
+    """XOR CPU baseline beside the XOR leg (BASELINE.json configs[1]):
+    redset_xor_encode_pthreads (src/redset_xor_pthreads.c:311-392) for the
+    encode and the serial rebuild (src/redset_xor_serial.c:161-275), as
+    restated in oracle/, on the XOR leg's own shape (p=8, 64 MiB cells)."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import numpy as np
+    import oracle_lib
+
+    oracle_lib.build()
+    rng = np.random.default_rng(8)
+    lofi = [_host_random((p - 1) * chunk, rng) for _ in range(p)]
+    xorc = [np.zeros(chunk, np.uint8) for _ in range(p)]
+    passes, t_enc, t_reb, threads = 0, 0.0, 0.0, 0
+    t_start = time.perf_counter()
+    while True:
+        t0 = time.perf_counter()
+        threads = oracle_lib.xor_encode_pthreads(p, lofi, xorc, chunk, slice_bytes=MIB)
+        t1 = time.perf_counter()
+        lf = [x if r != root else np.zeros_like(x) for r, x in enumerate(lofi)]
+        xc = [x if r != root else np.zeros_like(x) for r, x in enumerate(xorc)]
+        oracle_lib.xor_rebuild_set(p, root, lf, xc, chunk, slice_bytes=MIB)
+        t2 = time.perf_counter()
+        t_enc += t1 - t0
+        t_reb += t2 - t1
+        passes += 1
+        if time.perf_counter() - t_start >= target_s:
+            break
+    ok = np.array_equal(lf[root], lofi[root]) and np.array_equal(xc[root], xorc[root])
+    nbytes = p * p * chunk * passes  # p cells per stripe, p stripes, both passes
+    return {
+        "value": round(2 * nbytes / (t_enc + t_reb) / 1e9, 4),
+        "unit": "GB/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{passes} x (XOR p={p} full-set encode with {threads} pthreads + serial rebuild of member "
+                   f"{root}), chunk={chunk / MIB:g} MiB (host buffers, the XOR leg's shape); encode "
+                   f"{nbytes / t_enc / 1e9:.3f} GB/s, rebuild {nbytes / t_reb / 1e9:.3f} GB/s"),
+        "encode_GBps": round(nbytes / t_enc / 1e9, 4),
+        "rebuild_GBps": round(nbytes / t_reb / 1e9, 4),
+        "round_trip_equal": bool(ok),
     }
 
 
@@ -352,10 +410,14 @@ def emit(result, rank):
         _PRINTED.set()
 
 
+WATCHDOG_EXIT = 3
+
+
 def sharded_expired(result, rank, limit):
     """Watchdog of the sharded leg and the final barrier: print the line
-    measured so far if it is not out yet, then end this rank (the process
-    group is left hung, not torn down)."""
+    measured so far if it is not out yet, then end this rank with a non-zero
+    status (WATCHDOG_EXIT), so a hung exchange or barrier never looks like a
+    clean run to the caller (the process group is left hung, not torn down)."""
     with _PRINT_LOCK:
         if not _PRINTED.is_set():
             result["sharded"] = {"error": f"timed out after {limit:g} s"}
@@ -363,7 +425,7 @@ def sharded_expired(result, rank, limit):
                 print(json.dumps(result), flush=True)
             _PRINTED.set()
         print(f"rank {rank}: sharded leg or final barrier timed out after {limit:g} s", file=sys.stderr, flush=True)
-        os._exit(0)
+        os._exit(WATCHDOG_EXIT)
 
 
 def main():
@@ -395,6 +457,7 @@ def main():
     d = p - e
     chunk = int(args.chunk_mib * MIB)
     lost = sorted(int(x) for x in args.lost.split(",") if x != "")
+    cpu_chunk = int(args.cpu_chunk_mib * MIB) if args.cpu_chunk_mib > 0 else chunk
     stream = torch.cuda.current_stream()
 
     # this rank's own set, all cells resident in HBM
@@ -512,22 +575,26 @@ def main():
         result["rebuild_every_pair"] = rebuild_pairs(codec, lay, chunk, stream)
     if args.xor and rank == 0:
         result["xor"] = xor_leg(args, chunk, stream)
+        if args.cpu_baseline and not dist_on:
+            result["xor"]["cpu_baseline"] = cpu_baseline_xor(8, 3, args.cpu_seconds / 2, cpu_chunk)
     watchdog = None
-    if dist_on and args.sharded:
-        # second leg: the multi-rank rebuild with its RCCL exchange. It must
-        # not cost the main line: a failure is reported in "sharded" (every
-        # rank runs the same collectives, so they fail alike). A hung exchange
-        # cannot raise: a watchdog then prints the main line with the leg
-        # marked timed out and ends every rank.
+    if dist_on:
+        # A hung exchange or final barrier cannot raise: a watchdog then
+        # prints the main line (with the sharded leg marked timed out) and
+        # ends every rank with a non-zero status.
         watchdog = threading.Timer(args.sharded_timeout, sharded_expired, (result, rank, args.sharded_timeout))
         watchdog.daemon = True
         watchdog.start()
+    if dist_on and args.sharded:
+        # second leg: the multi-rank rebuild with its RCCL exchange. It must
+        # not cost the main line: a failure is reported in "sharded" (every
+        # rank runs the same collectives, so they fail alike).
         try:
             result["sharded"] = sharded_leg(args, p, e, chunk, lost, world, rank)
         except Exception as exc:  # noqa: BLE001 -- reported, not swallowed
             result["sharded"] = {"error": f"{type(exc).__name__}: {exc}"}
     if args.cpu_baseline and rank == 0 and not dist_on:
-        result["cpu_baseline"] = cpu_baseline(p, e, lost, args.cpu_seconds)
+        result["cpu_baseline"] = cpu_baseline(p, e, lost, args.cpu_seconds, cpu_chunk)
     emit(result, rank)
     if dist_on:
         dist.barrier()

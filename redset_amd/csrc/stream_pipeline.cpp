@@ -185,6 +185,14 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
       cv.wait(lk, [&] { return S.state == want || abort.load(); });
       return !abort.load();
     };
+    // wake every stage and make it return (a HIP failure anywhere)
+    auto stop = [&] {
+      {
+        std::lock_guard<std::mutex> g(mu);
+        abort = true;
+      }
+      cv.notify_all();
+    };
     auto set_state = [&](Slot& S, SlotState s) {
       {
         std::lock_guard<std::mutex> g(mu);
@@ -229,7 +237,14 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
       for (size_t u = 0; u < nunits; ++u) {
         Slot& S = slots[u % kSlots];
         if (!wait_state(S, kOnGpu)) return;
-        if (hipEventSynchronize(S.ev_done) != hipSuccess) io_err = 2;
+        if (hipEventSynchronize(S.ev_done) != hipSuccess) {
+          io_err = 2;
+          stop();
+          return;
+        }
+        // the pipeline failed after this unit was published: do not write
+        // bytes that may belong to no finished computation
+        if (abort.load()) return;
         float ms = 0;
         if (hipEventElapsedTime(&ms, S.ev_start, S.ev_done) == hipSuccess) gpu_s += ms * 1e-3;
         const Unit& U = units[u];
@@ -277,19 +292,15 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
         rc = hip_ok(hipMemcpyAsync(to, S.d_out + j * slice, U.len, hipMemcpyDeviceToHost, s_out), "D2H");
       }
       rc = rc ? rc : hip_ok(hipEventRecord(S.ev_done, s_out), "event record");
+      // a failed unit is never handed to the writer (its ev_done may not be
+      // recorded and h_out would hold another unit's bytes): abort below
+      if (rc != 0) break;
       st.bytes_read += nin * U.len;
       st.bytes_written += nout * U.len;
       st.units += 1;
       set_state(S, kOnGpu);
     }
-    if (rc != 0) {
-      // a HIP failure: stop the reader and writer wherever they wait
-      {
-        std::lock_guard<std::mutex> g(mu);
-        abort = true;
-      }
-      cv.notify_all();
-    }
+    if (rc != 0) stop();  // a HIP failure: stop the reader and writer wherever they wait
     reader.join();
     writer.join();
   }
@@ -315,6 +326,7 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
   st.gpu_seconds = gpu_s;
   if (stats) *stats = st;
   if (rc) return rc;
+  if (io_err.load() == 2) return fail("stream pipeline: device-to-host copy failed");
   if (io_err.load()) return fail("stream I/O callback failed");
   return REDSET_SUCCESS;
 }
@@ -384,7 +396,11 @@ struct redset_hip_fileio {
 namespace {
 
 // pread/pwrite of a full range, retrying short transfers and EINTR
-// (redset_read_attempt / redset_write_attempt, src/redset_io.c:234-310)
+// (redset_read_attempt / redset_write_attempt, src/redset_io.c:234-310).
+// EOF inside the range is a failure, as a short redset_read_attempt is to
+// its callers (src/redset_lofi.c:74-77, src/redset_reedsolomon.c:678-681):
+// a data or redundancy file shorter than recorded must not read as zeros.
+// Zero padding exists only past a member's last file (lofi_rw).
 int full_pread(int fd, void* buf, size_t len, off_t off) {
   char* p = static_cast<char*>(buf);
   while (len > 0) {
@@ -393,10 +409,7 @@ int full_pread(int fd, void* buf, size_t len, off_t off) {
       if (errno == EINTR) continue;
       return -1;
     }
-    if (n == 0) {  // EOF: zero fill (logical file padding)
-      std::memset(p, 0, len);
-      return 0;
-    }
+    if (n == 0) return -1;  // EOF before the end of the recorded range
     p += n;
     len -= static_cast<size_t>(n);
     off += n;

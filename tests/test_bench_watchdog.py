@@ -1,5 +1,6 @@
 """bench.py's sharded-leg watchdog (host logic only, no GPU): a hung RCCL
-exchange must still leave rank 0's one JSON line on stdout, printed once."""
+exchange must still leave rank 0's one JSON line on stdout, printed once, and
+end the process with a non-zero status (a hang is never a clean run)."""
 import json
 import os
 import subprocess
@@ -17,7 +18,7 @@ def test_expired_leg_prints_main_line_and_exits():
              "bench.sharded_expired({'metric': 'm', 'value': 1.0}, 0, 2.0)\n"
              "time.sleep(5)\n"
              "print('not reached')\n")
-    assert r.returncode == 0
+    assert r.returncode == 3
     lines = r.stdout.strip().splitlines()
     assert len(lines) == 1
     line = json.loads(lines[0])
@@ -29,7 +30,7 @@ def test_watchdog_after_print_exits_without_second_line():
              "res = {'metric': 'm', 'value': 2.0, 'sharded': {'value': 3.0}}\n"
              "bench.emit(res, 0)\n"
              "bench.sharded_expired(res, 0, 1.0)\n")
-    assert r.returncode == 0
+    assert r.returncode == 3
     lines = r.stdout.strip().splitlines()
     assert len(lines) == 1 and json.loads(lines[0])["sharded"] == {"value": 3.0}
     assert "timed out" in r.stderr
@@ -37,4 +38,4 @@ def test_watchdog_after_print_exits_without_second_line():
 
 def test_other_ranks_print_nothing():
     r = _run("import bench\nbench.sharded_expired({'value': 1.0}, 3, 1.0)\n")
-    assert r.returncode == 0 and r.stdout == ""
+    assert r.returncode == 3 and r.stdout == ""

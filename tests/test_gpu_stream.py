@@ -194,3 +194,40 @@ def test_stream_direct_dma_pinned(rd, oracle, p, e, chunk):
         buf[r * per:(r + 1) * per].zero_()
     stream.rs_rebuild_stream(codec, [0, 7], chunk, io, slice_bytes=1 << 16)
     assert torch.equal(buf, ref)
+
+
+@pytest.mark.parametrize("victim", ["data", "parity"])
+def test_short_survivor_file_fails_the_rebuild(rd, oracle, tmp_path, victim):
+    """A survivor's data file or redundancy file that is shorter than its
+    recorded size must fail the rebuild, as a short redset_read_attempt does
+    (src/redset_lofi.c:74-77, src/redset_reedsolomon.c:678-681), instead of
+    reading as zeros and reporting success with wrong bytes. Zero padding
+    applies only past a member's last file."""
+    redset_amd, stream = rd
+    rng = np.random.default_rng(5)
+    p, e = 6, 2
+    tmp = str(tmp_path)
+    files = [_write_member_files(tmp, r, rng, nfiles=2, maxsize=100_000) for r in range(p)]
+    chunk = stream.chunk_size_for(max(sum(s for _, s in f) for f in files), p - e)
+    header = [512] * p
+    reds = [os.path.join(tmp, f"rank{r}.rs.redset") for r in range(p)]
+    codec = redset_amd.RSCodec(p, e)
+    io = stream.FileIO(files, reds, header, chunk)
+    stream.rs_encode_stream(codec, chunk, io, slice_bytes=16384)
+    io.close()
+    lost = [1]
+    for path, _ in files[1]:
+        os.unlink(path)
+    os.unlink(reds[1])
+    survivor = 3
+    if victim == "data":
+        path, size = max(files[survivor], key=lambda f: f[1])
+        assert size > 10
+        os.truncate(path, size // 2)
+    else:
+        # slot 0 = stripe 3, whose rebuild of member 1's data reads it (row 0)
+        os.truncate(reds[survivor], header[survivor] + chunk // 2)
+    io = stream.FileIO(files, reds, header, chunk, writable=[r in lost for r in range(p)])
+    with pytest.raises(redset_amd.RedsetHipError, match="I/O"):
+        stream.rs_rebuild_stream(codec, lost, chunk, io, slice_bytes=16384)
+    io.close()

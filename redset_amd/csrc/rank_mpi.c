@@ -25,6 +25,7 @@
 
 #define DEFAULT_BUF ((size_t) 1 << 20) /* redset_mpi_buf_size default, src/redset.c:45 */
 #define MAX_SCRATCH 8
+#define MAX_STAGE ((size_t) 64 << 20) /* RS encode: bytes of ring slices staged per window */
 
 static int fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 static int fail(const char* fmt, ...) {
@@ -126,6 +127,32 @@ static int pwrite_full(int fd, const void* buf, size_t n, off_t off) {
   return 0;
 }
 
+/* Every member must enter the exchange loop or none may: a member whose
+ * setup failed (scratch allocation, decode map) would otherwise leave its
+ * peers blocked in the ring. One MPI_Allreduce(LAND) over the setup result,
+ * as redset's callers AND-reduce a backend's rc (redset_alltrue,
+ * src/redset_reedsolomon.c:1132). */
+static int agree_setup(MPI_Comm comm, int rc) {
+  int ok = rc == 0, all = 0;
+  if (MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_LAND, comm) != MPI_SUCCESS) return fail("MPI_Allreduce failed");
+  if (!all) return rc ? rc : fail("a peer's setup failed");
+  return 0;
+}
+
+/* Test hook: REDSET_HIP_INJECT_DEVICE_FAILURE=<rank> makes that rank's first
+ * device step report a failure (tests/mpi/rank_test.c drives it), so the
+ * keep-the-collective-going path below is exercised without a broken GPU. */
+static int injected_device_failure(MPI_Comm comm) {
+  static int fired = 0;
+  const char* v = getenv("REDSET_HIP_INJECT_DEVICE_FAILURE");
+  int r = -1;
+  if (!v || fired) return 0;
+  MPI_Comm_rank(comm, &r);
+  if (atoi(v) != r) return 0;
+  fired = 1;
+  return fail("injected device failure (REDSET_HIP_INJECT_DEVICE_FAILURE)");
+}
+
 static int comm_geometry(MPI_Comm comm, int* ranks, int* rank) {
   if (MPI_Comm_size(comm, ranks) != MPI_SUCCESS || MPI_Comm_rank(comm, rank) != MPI_SUCCESS)
     return fail("MPI_Comm_size/rank failed");
@@ -144,6 +171,7 @@ static int xor_segment(int t, int c) { return c < t ? c : c - 1; }
 
 /* ---- RS encode (replaces redset_reedsolomon_encode, src/redset_reedsolomon.c:280-402) */
 
+
 int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi,
                               const char* chunk_file, int fd_chunk, size_t chunk_size, size_t buf_size) {
   int p, r, rp, e;
@@ -151,25 +179,33 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
   if (!rs || !lofi || !lofi->read) return fail("rs_encode_rank: null argument");
   if (comm_geometry(comm, &p, &r) || redset_hip_rs_shape(rs, &rp, &e)) return REDSET_FAILURE;
   if (p != rp) return fail("communicator has %d ranks, codec %d", p, rp);
-  if (header_size(fd_chunk, chunk_file, &header)) return REDSET_FAILURE;
+  /* a bad fd on one member is agreed on below, not returned early: its
+   * peers would wait for it in the first collective */
+  const int hrc = header_size(fd_chunk, chunk_file, &header);
   const int d = p - e;
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+  /* ring steps staged per window: the d*e slices of a slice's whole ring
+   * would need d*e*B of pinned and device memory (O(p*e)); windows of G steps
+   * bound it to MAX_STAGE, the reference's own scratch being e+e+1 slices */
+  int G = (int) (MAX_STAGE / ((size_t) e * B));
+  if (G < 1) G = 1;
+  if (G > d) G = d;
 
   unsigned char* mat = malloc((size_t) (p + e) * p);
   unsigned char* coef = malloc((size_t) e * d);       /* [slot i][ring step s] */
-  const unsigned char** ins = malloc(sizeof(*ins) * (size_t) d);
+  const unsigned char** ins = malloc(sizeof(*ins) * (size_t) G);
   MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) e);
   scratch S;
   scratch_init(&S);
   uint8_t* h_send = scratch_host(&S, B);
-  uint8_t* h_recv = scratch_host(&S, (size_t) d * e * B); /* [step s][slot i] */
+  uint8_t* h_recv = scratch_host(&S, (size_t) G * e * B); /* [step in window][slot i] */
   uint8_t* h_par = scratch_host(&S, (size_t) e * B);
-  uint8_t* d_recv = scratch_dev(&S, (size_t) d * e * B);
+  uint8_t* d_recv = scratch_dev(&S, (size_t) G * e * B);
   uint8_t* d_par = scratch_dev(&S, (size_t) e * B);
-  int rc = S.rc;
+  int rc = S.rc ? S.rc : hrc;
   if (!rc && (!mat || !coef || !ins || !req)) rc = fail("out of host memory");
   if (!rc) rc = redset_hip_rs_matrix(rs, mat);
-  if (rc) goto out;
+  if ((rc = agree_setup(comm, rc))) goto out;
 
   /* slot i's coefficients over the d slices it receives, in ring-step order:
    * at step s (chunk_step p-1-s) slot i receives from r + (p - chunk_step + i) */
@@ -180,33 +216,53 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
       coef[(size_t) i * d + s] = mat[(size_t) (p + i) * p + sender];
     }
 
+  /* after a device failure the loop keeps every MPI call (peers must not
+   * hang, src/redset_reedsolomon.c:338-342) but skips GPU work and writes */
+  int dev_failed = 0;
   for (size_t nread = 0; nread < chunk_size; nread += B) {
     const size_t count = min_sz(B, chunk_size - nread);
-    for (int s = 0; s < d; ++s) { /* chunk_step = p-1 .. e, src/redset_reedsolomon.c:329-377 */
-      const int step = p - 1 - s;
-      const int chunk_id = (r + step) % p;
-      const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
-      if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0) rc = fail("lofi read failed");
-      int k = 0;
-      for (int i = 0; i < e; ++i) {
-        const int dist = p - step + i;
-        MPI_Irecv(h_recv + ((size_t) s * e + i) * B, (int) count, MPI_BYTE, (r + dist) % p, 0, comm, &req[k++]);
-        MPI_Isend(h_send, (int) count, MPI_BYTE, (r - dist + p) % p, 0, comm, &req[k++]);
+    for (int s0 = 0; s0 < d; s0 += G) {
+      const int gs = d - s0 < G ? d - s0 : G;
+      for (int s = s0; s < s0 + gs; ++s) { /* chunk_step = p-1 .. e, src/redset_reedsolomon.c:329-377 */
+        const int step = p - 1 - s;
+        const int chunk_id = (r + step) % p;
+        const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
+        if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0) {
+          rc = fail("lofi read failed");
+          memset(h_send, 0, count);
+        }
+        int k = 0;
+        for (int i = 0; i < e; ++i) {
+          const int dist = p - step + i;
+          MPI_Irecv(h_recv + ((size_t) (s - s0) * e + i) * B, (int) count, MPI_BYTE, (r + dist) % p, 0, comm,
+                    &req[k++]);
+          MPI_Isend(h_send, (int) count, MPI_BYTE, (r - dist + p) % p, 0, comm, &req[k++]);
+        }
+        MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
       }
-      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+      if (dev_failed) continue;
+      /* the window's gs*e slices: one H2D, one kernel per slot accumulating
+       * over the window's steps, then wait before h_recv is reused */
+      int grc = injected_device_failure(comm);
+      if (!grc) grc = h2d(&S, d_recv, h_recv, (size_t) gs * e * B);
+      for (int i = 0; i < e && !grc; ++i) {
+        for (int s = 0; s < gs; ++s) ins[s] = d_recv + ((size_t) s * e + i) * B;
+        unsigned char* o = d_par + (size_t) i * B;
+        grc = redset_hip_gf_combine(ins, gs, &o, 1, coef + (size_t) i * d + s0, count, s0 > 0, S.stream);
+      }
+      if (!grc) grc = sync_stream(&S);
+      if (grc) {
+        rc = grc;
+        dev_failed = 1;
+      }
     }
-    /* all d*e slices of this window: one H2D, one kernel per slot, one D2H */
-    int grc = h2d(&S, d_recv, h_recv, (size_t) d * e * B);
-    for (int i = 0; i < e && !grc; ++i) {
-      for (int s = 0; s < d; ++s) ins[s] = d_recv + ((size_t) s * e + i) * B;
-      unsigned char* o = d_par + (size_t) i * B;
-      grc = redset_hip_gf_combine(ins, d, &o, 1, coef + (size_t) i * d, count, 0, S.stream);
-    }
-    if (!grc) grc = d2h(&S, h_par, d_par, (size_t) e * B);
+    if (dev_failed) continue;
+    int grc = d2h(&S, h_par, d_par, (size_t) e * B);
     if (!grc) grc = sync_stream(&S);
-    if (grc) { /* a device failure is not recoverable mid-collective */
+    if (grc) {
       rc = grc;
-      goto out;
+      dev_failed = 1;
+      continue;
     }
     for (int i = 0; i < e; ++i) { /* :379-388 */
       const off_t off = header + (off_t) i * (off_t) chunk_size + (off_t) nread;
@@ -233,7 +289,9 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   if (comm_geometry(comm, &p, &r) || redset_hip_rs_shape(rs, &rp, &e)) return REDSET_FAILURE;
   if (p != rp) return fail("communicator has %d ranks, codec %d", p, rp);
   if (missing < 1 || missing > e) return fail("cannot rebuild %d members with %d encoding blocks", missing, e);
-  if (header_size(fd_chunk, chunk_file, &header)) return REDSET_FAILURE;
+  /* a bad fd on one member is agreed on below, not returned early: its
+   * peers would wait for it in the first collective */
+  const int hrc = header_size(fd_chunk, chunk_file, &header);
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
 
   unsigned char* D = malloc((size_t) missing * p); /* decode map of stripe r: missing x p */
@@ -250,12 +308,12 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   uint8_t* h_gather = scratch_host(&S, (size_t) p * B); /* rebuilt cells from every solver */
   uint8_t* d_cells = scratch_dev(&S, (size_t) p * B);
   uint8_t* d_out = scratch_dev(&S, (size_t) missing * B);
-  int rc = S.rc;
+  int rc = S.rc ? S.rc : hrc;
   if (!rc && (!D || !coef || !cols || !ins || !outs || !req)) rc = fail("out of host memory");
   /* member r solves stripe r (decode_chunk_id = rank, :607-611): one linear
    * map equal to redset_rs_reduce_decode + redset_rs_gaussian_solve */
   if (!rc) rc = redset_hip_rs_decode_matrix(rs, missing, rebuild_ranks, r, D);
-  if (rc) goto out;
+  if ((rc = agree_setup(comm, rc))) goto out;
   int ncols = 0;
   for (int s = 0; s < p; ++s) {
     int used = 0;
@@ -267,6 +325,10 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   for (int k = 0; k < ncols; ++k) ins[k] = d_cells + (size_t) cols[k] * B;
   for (int i = 0; i < missing; ++i) outs[i] = d_out + (size_t) i * B;
 
+  /* after a device failure every MPI call of the loop still runs (peers must
+   * not hang, src/redset_reedsolomon.c:666-681 keep going on read errors);
+   * this member then sends zeros as its solved cells and fails the call */
+  int dev_failed = 0;
   for (size_t nread = 0; nread < chunk_size; nread += B) {
     const size_t count = min_sz(B, chunk_size - nread);
     for (int step = 0; step < p; ++step) { /* :646-703 */
@@ -274,14 +336,17 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
       const int chunk_id = (r + step) % p;
       const int enc = redset_hip_rs_get_encoding_id(p, e, r, chunk_id);
       if (!need_rebuild) {
+        int bad;
         if (enc < p) {
           const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
-          if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0)
-            rc = fail("lofi read failed");
+          bad = lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0;
+          if (bad) rc = fail("lofi read failed");
         } else {
           const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) nread;
-          if (pread_full(fd_chunk, h_send, count, off) != 0) rc = fail("read %s failed", chunk_file);
+          bad = pread_full(fd_chunk, h_send, count, off) != 0;
+          if (bad) rc = fail("read %s failed", chunk_file);
         }
+        if (bad) memset(h_send, 0, count);
       } else {
         memset(h_send, 0, count); /* an erased member contributes nothing */
       }
@@ -293,14 +358,18 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
         memcpy(h_cells + (size_t) r * B, h_send, count);
       }
     }
-    int grc = h2d(&S, d_cells, h_cells, (size_t) p * B);
-    if (!grc && ncols > 0) grc = redset_hip_gf_combine(ins, ncols, outs, missing, coef, count, 0, S.stream);
-    if (!grc) grc = d2h(&S, h_out, d_out, (size_t) missing * B);
-    if (!grc) grc = sync_stream(&S);
-    if (grc) {
-      rc = grc;
-      goto out;
+    if (!dev_failed) {
+      int grc = injected_device_failure(comm);
+      if (!grc) grc = h2d(&S, d_cells, h_cells, (size_t) p * B);
+      if (!grc && ncols > 0) grc = redset_hip_gf_combine(ins, ncols, outs, missing, coef, count, 0, S.stream);
+      if (!grc) grc = d2h(&S, h_out, d_out, (size_t) missing * B);
+      if (!grc) grc = sync_stream(&S);
+      if (grc) {
+        rc = grc;
+        dev_failed = 1;
+      }
     }
+    if (dev_failed) memset(h_out, 0, (size_t) missing * B);
     /* gather rebuilt cells to the erased members, :713-733 */
     int k = 0;
     if (need_rebuild)
@@ -347,7 +416,9 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
   if (!lofi || !lofi->read) return fail("xor_encode_rank: null argument");
   if (comm_geometry(comm, &p, &r)) return REDSET_FAILURE;
   if (p < 2) return fail("XOR needs at least 2 ranks");
-  if (header_size(fd_chunk, chunk_file, &header)) return REDSET_FAILURE;
+  /* a bad fd on one member is agreed on below, not returned early: its
+   * peers would wait for it in the first collective */
+  const int hrc = header_size(fd_chunk, chunk_file, &header);
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
 
   const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
@@ -359,12 +430,13 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
   uint8_t* h_out = scratch_host(&S, B);
   uint8_t* d_recv = scratch_dev(&S, (size_t) p * B);
   uint8_t* d_out = scratch_dev(&S, B);
-  int rc = S.rc;
+  int rc = S.rc ? S.rc : hrc;
   if (!rc && (!ins || !req)) rc = fail("out of host memory");
-  if (rc) goto out;
+  if ((rc = agree_setup(comm, rc))) goto out;
   int nin = 0;
   for (int t = 0; t < p; ++t)
     if (t != r) ins[nin++] = d_recv + (size_t) t * B;
+  int dev_failed = 0; /* then keep exchanging, skip GPU work and writes */
 
   for (size_t nread = 0; nread < chunk_size; nread += B) {
     const size_t count = min_sz(B, chunk_size - nread);
@@ -373,19 +445,24 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
      * every other member's cell of stripe r; exchange those cells directly */
     for (int t = 0; t < p; ++t) {
       if (t == r) continue;
-      if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, t), nread, count, h_send + (size_t) t * B) != 0)
+      if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, t), nread, count, h_send + (size_t) t * B) != 0) {
         rc = fail("lofi read failed");
+        memset(h_send + (size_t) t * B, 0, count);
+      }
       MPI_Irecv(h_recv + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
       MPI_Isend(h_send + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
     }
     MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
-    int grc = h2d(&S, d_recv, h_recv, (size_t) p * B);
+    if (dev_failed) continue;
+    int grc = injected_device_failure(comm);
+    if (!grc) grc = h2d(&S, d_recv, h_recv, (size_t) p * B);
     if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out, count, 0, S.stream);
     if (!grc) grc = d2h(&S, h_out, d_out, count);
     if (!grc) grc = sync_stream(&S);
     if (grc) {
       rc = grc;
-      goto out;
+      dev_failed = 1;
+      continue;
     }
     if (pwrite_full(fd_chunk, h_out, count, header + (off_t) nread) != 0) /* :280-284 */
       rc = fail("write %s failed", chunk_file);
@@ -406,7 +483,9 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   if (!lofi || !lofi->read) return fail("xor_decode_rank: null argument");
   if (comm_geometry(comm, &p, &r)) return REDSET_FAILURE;
   if (root < 0 || root >= p) return fail("root %d out of range", root);
-  if (header_size(fd_chunk, chunk_file, &header)) return REDSET_FAILURE;
+  /* a bad fd on one member is agreed on below, not returned early: its
+   * peers would wait for it in the first collective */
+  const int hrc = header_size(fd_chunk, chunk_file, &header);
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
 
   const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
@@ -417,12 +496,13 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   uint8_t* h_out = scratch_host(&S, B);
   uint8_t* d_cells = scratch_dev(&S, (size_t) p * B);
   uint8_t* d_out = scratch_dev(&S, B);
-  int rc = S.rc;
+  int rc = S.rc ? S.rc : hrc;
   if (!rc && (!ins || !req)) rc = fail("out of host memory");
-  if (rc) goto out;
+  if ((rc = agree_setup(comm, rc))) goto out;
   int nin = 0;
   for (int t = 0; t < p; ++t)
     if (t != root) ins[nin++] = d_cells + (size_t) t * B;
+  int dev_failed = 0; /* root: keep receiving every cell, skip GPU work and writes */
 
   /* stripe by stripe, as the reference's pipelined reduce to the root
    * (src/redset_xor.c:466-524): every survivor sends its cell of stripe c,
@@ -432,12 +512,15 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
       const size_t count = min_sz(B, chunk_size - nread);
       if (r != root) {
         uint8_t* mine = h_cells + (size_t) r * B;
+        int bad;
         if (c != r) {
-          if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, c), nread, count, mine) != 0)
-            rc = fail("lofi read failed");
-        } else if (pread_full(fd_chunk, mine, count, header + (off_t) nread) != 0) {
-          rc = fail("read %s failed", chunk_file);
+          bad = lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, c), nread, count, mine) != 0;
+          if (bad) rc = fail("lofi read failed");
+        } else {
+          bad = pread_full(fd_chunk, mine, count, header + (off_t) nread) != 0;
+          if (bad) rc = fail("read %s failed", chunk_file);
         }
+        if (bad) memset(mine, 0, count);
         MPI_Send(mine, (int) count, MPI_BYTE, root, 0, comm);
         continue;
       }
@@ -445,13 +528,16 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
       for (int t = 0; t < p; ++t)
         if (t != root) MPI_Irecv(h_cells + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
       MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
-      int grc = h2d(&S, d_cells, h_cells, (size_t) p * B);
+      if (dev_failed) continue;
+      int grc = injected_device_failure(comm);
+      if (!grc) grc = h2d(&S, d_cells, h_cells, (size_t) p * B);
       if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out, count, 0, S.stream);
       if (!grc) grc = d2h(&S, h_out, d_out, count);
       if (!grc) grc = sync_stream(&S);
       if (grc) {
         rc = grc;
-        goto out;
+        dev_failed = 1;
+        continue;
       }
       if (c != root) {
         if (!lofi->write ||

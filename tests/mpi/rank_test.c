@@ -9,6 +9,8 @@
  * Rank r reads <dir>/manifest_<r>.txt:
  *   nfiles \n path size \n ... chunk_size \n header_size \n redundancy_path
  * (written by tests/test_gpu_mpi.py). Exit 0 iff every rank succeeded.
+ * RANK_TEST_FAIL_READ=<rank>: that rank's logical-file reads fail from the
+ * second call on (an I/O error in the middle of the collective loop).
  */
 #include <fcntl.h>
 #include <mpi.h>
@@ -19,6 +21,14 @@
 
 #include "redset_hip.h"
 #include "redset_hip_mpi.h"
+
+/* logical-file reads that start failing mid-loop (fault injection) */
+static redset_hip_io inner_io;
+static int reads_done = 0;
+static int failing_read(void* ctx, int rank, int kind, int index, unsigned long long off, size_t len, void* dst) {
+  if (reads_done++ >= 1) return -1;
+  return inner_io.read(ctx, rank, kind, index, off, len, dst);
+}
 
 int main(int argc, char** argv) {
   MPI_Init(&argc, &argv);
@@ -68,6 +78,12 @@ int main(int argc, char** argv) {
   if (rc != REDSET_SUCCESS) {
     fprintf(stderr, "rank %d: fileio: %s\n", rank, redset_hip_last_error());
     MPI_Abort(MPI_COMM_WORLD, 4);
+  }
+
+  const char* fr = getenv("RANK_TEST_FAIL_READ");
+  if (fr && atoi(fr) == rank) {
+    inner_io = io;
+    io.read = failing_read;
   }
 
   /* redundancy file: header first, backend writes after it */

@@ -109,3 +109,45 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf):
             assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
         blob = np.fromfile(reds[r], dtype=np.uint8)
         assert np.array_equal(blob[header[r]:header[r] + e * chunk], want[r]), r
+
+
+@pytest.mark.parametrize("scheme,op,env", [
+    ("rs", "encode", {"RANK_TEST_FAIL_READ": "2"}),
+    ("rs", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "1"}),
+    ("rs", "rebuild", {"RANK_TEST_FAIL_READ": "3"}),
+    ("rs", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "0"}),
+    ("xor", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2"}),
+    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "1"}),
+    ("xor", "rebuild", {"RANK_TEST_FAIL_READ": "0"}),
+])
+def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme, op, env):
+    """One member's I/O or device error in the middle of the loop: that member
+    keeps every MPI call of the collective going (as src/redset_reedsolomon.c:
+    338-342 does on read errors), returns REDSET_FAILURE, and the caller's
+    AND-reduce (redset_alltrue) fails every rank. No rank may hang."""
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    tmp = str(tmp_path)
+    p, e = (4, 2) if scheme == "rs" else (4, 1)
+    d = p - e
+    rng = np.random.default_rng(3)
+    files, chunk = _setup(tmp, p, d, rng, 300_000)
+    header = [512] * p
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, header, reds)
+    buf = 16384  # several slices per chunk: the failure lands mid-loop
+    if op == "rebuild":
+        res = _mpirun(p, [scheme, "encode", e, tmp, buf])
+        assert res.returncode == 0, res.stdout + res.stderr
+        lost = [1] if scheme == "rs" else [2]
+        for r in lost:
+            for path, _ in files[r]:
+                os.unlink(path)
+            os.unlink(reds[r])
+        args = [scheme, "rebuild", e, tmp, buf] + lost
+    else:
+        args = [scheme, "encode", e, tmp, buf]
+    cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST] + [str(a) for a in args]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=90, env={**os.environ, **env})
+    assert res.returncode != 0, res.stdout + res.stderr  # every rank exits 1 (alltrue is false)
+    assert "backend failed" in res.stderr

@@ -217,6 +217,125 @@ int redset_hip_fileio_create(int ranks, const int* nfiles, const char* const* pa
                              redset_hip_io* io_out, redset_hip_fileio** out);
 void redset_hip_fileio_destroy(redset_hip_fileio* f);
 
+/* ---- sets sharded over the GPUs of a node (multi-rank rebuild) ------- */
+/*
+ * Replaces the reference's MPI rings for a redundancy set whose members live
+ * on different GPUs: the decode's reduce ring (src/redset_reedsolomon.c:
+ * 646-703) becomes ONE grouped exchange that gathers, onto every GPU, its
+ * column slice of each cell the decode reads; every GPU runs the gf_mac
+ * kernel on its slice of every stripe; a second grouped exchange returns the
+ * rebuilt slices to the GPUs hosting the lost members (the gather of :713-733).
+ * Byte j of an output depends only on byte j of its stripe's inputs
+ * (SURVEY.md §8e), so the column slices are independent. Encode works the
+ * same way (all data cells in, all parity cells back; replaces :329-377).
+ *
+ * World: `world` processes (one per GPU), this one is `rank`. The caller
+ * places `nsets` sets of p members: member r of set k is hosted by process
+ * host[k*p + r] at hosted index slot[k*p + r] (< max_hosted). Every cell is
+ * cut into `world` column slices of `slice_bytes` (W) bytes
+ * (redset_hip_shard_slice_bytes); slice q covers cell bytes [q*W, q*W + W)
+ * clipped to chunk_size. Buffers of this process (device memory for the HIP
+ * compute and RCCL; any memory the transport and compute can address):
+ *   hosted_data     [world][max_hosted][d][W]   slice q of data cell s of my
+ *                                               hosted member j
+ *   hosted_parity   [world][max_hosted][e][W]   same for parity slot i
+ *   gathered_data   [world][max_hosted][d][W]   my slice of data cell s of the
+ *                                               member hosted at (h, j)
+ *   gathered_parity [world][max_hosted][e][W]
+ * (d = p - e). A member's logical file is thus stored as `world` column slabs.
+ */
+typedef struct {
+  int peer;     /* process in the transport's world; == own rank: a local copy */
+  int send;     /* 1: send buf to peer; 0: receive buf from peer (local copy:
+                   the send entry is the source, the receive entry right after
+                   it the destination) */
+  void* buf;
+  size_t len;
+} redset_hip_xfer;
+
+typedef struct {
+  int world, rank;
+  /* Run one exchange: every transfer of the list concurrently (sends and
+   * receives between a pair of processes are listed in the same order on
+   * both sides, with equal lengths). Stream-ordered transports (RCCL) enqueue
+   * on `stream` and return; others complete before returning, after waiting
+   * for work already on `stream`. Return 0 on success. */
+  int (*exchange)(void* ctx, const redset_hip_xfer* xfers, int n, void* stream);
+  void* ctx;
+} redset_hip_transport;
+
+typedef struct {
+  /* Optional compute (NULL run = the HIP gf_mac plans): encode (kind
+   * REDSET_HIP_PLAN_RS_ENCODE) or rebuild (..._RS_REBUILD, `missing` erased
+   * members) of one set whose cells are at lofi/parity in the set layout
+   * (cell_stride apart, nbytes each). Tests put the CPU oracle here. */
+  int (*run)(void* ctx, int kind, int missing, const int* rebuild_ranks, unsigned char* const* lofi,
+             unsigned char* const* parity, size_t nbytes, size_t cell_stride, void* stream);
+  void* ctx;
+} redset_hip_compute;
+
+typedef struct {
+  int nsets;
+  const int* host;              /* [nsets * p] */
+  const int* slot;              /* [nsets * p] */
+  int max_hosted;
+  size_t chunk_size;
+  size_t slice_bytes;           /* W */
+  unsigned char* hosted_data;
+  unsigned char* hosted_parity;
+  unsigned char* gathered_data;
+  unsigned char* gathered_parity;
+} redset_hip_shard_layout;
+
+typedef struct {
+  int kind;                               /* REDSET_HIP_PLAN_RS_ENCODE / _REBUILD */
+  int world, rank, nsets, missing;
+  size_t my_slice_len;                    /* cell bytes of this process's slice */
+  int gather_messages, return_messages;   /* peer messages after merging (no local copies) */
+  unsigned long long gather_bytes_sent;   /* to other processes, per execute */
+  unsigned long long gather_bytes_recv;
+  unsigned long long return_bytes_sent;
+  unsigned long long return_bytes_recv;
+  unsigned long long local_bytes;         /* copied within this process */
+  unsigned long long compute_bytes;       /* algorithmic bytes of this process's slice */
+} redset_hip_sharded_info;
+
+typedef struct redset_hip_sharded redset_hip_sharded;
+
+enum { REDSET_HIP_PHASE_GATHER = 0, REDSET_HIP_PHASE_COMPUTE = 1, REDSET_HIP_PHASE_RETURN = 2 };
+
+/* Column slice width for chunk_size bytes over `world` processes: ceil(C/world)
+ * rounded up to 256 B (so every slice starts 16-B aligned). */
+size_t redset_hip_shard_slice_bytes(size_t chunk_size, int world);
+
+/* Plan the sharded encode (kind REDSET_HIP_PLAN_RS_ENCODE, missing 0) or
+ * rebuild of `missing` members (ascending rebuild_ranks, the same in every
+ * set) of every set. Collective in the sense that every process plans with
+ * the same placement; planning itself does no communication. The rebuild
+ * gathers only the cells some stripe's decode reads (surviving data and the
+ * parity rows identify_rows selects, src/redset_reedsolomon_common.c:
+ * 425-564) and never a lost member's. */
+int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
+                               const redset_hip_shard_layout* layout, const redset_hip_transport* transport,
+                               const redset_hip_compute* compute, redset_hip_sharded** out);
+/* All three phases (gather, compute, return) on `stream`. */
+int redset_hip_sharded_execute(redset_hip_sharded* plan, void* stream);
+/* One phase (REDSET_HIP_PHASE_*), so callers can time them apart. */
+int redset_hip_sharded_execute_phase(redset_hip_sharded* plan, int phase, void* stream);
+int redset_hip_sharded_get_info(const redset_hip_sharded* plan, redset_hip_sharded_info* info);
+void redset_hip_sharded_destroy(redset_hip_sharded* plan);
+
+/* RCCL transport over xGMI (grouped ncclSend / ncclRecv on the caller's
+ * stream; local copies as hipMemcpyAsync). One process calls
+ * redset_hip_rccl_unique_id, the caller distributes the 128 bytes (any
+ * channel: MPI_Bcast, torch.distributed, a file), then every process creates
+ * its transport collectively (ncclCommInitRank) on its current device. */
+typedef struct redset_hip_rccl redset_hip_rccl;
+int redset_hip_rccl_unique_id(unsigned char id_out[128]);
+int redset_hip_rccl_transport_create(const unsigned char id[128], int world, int rank, redset_hip_transport* out,
+                                     redset_hip_rccl** handle);
+void redset_hip_rccl_transport_destroy(redset_hip_rccl* handle);
+
 /* Text of the last failure on this thread ("" if none). */
 const char* redset_hip_last_error(void);
 /* For layers built on this library (the per-rank backends of

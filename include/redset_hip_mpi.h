@@ -50,6 +50,18 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
 int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
                                int fd_chunk, size_t chunk_size, size_t buf_size);
 
+/* Transport of the sharded path (redset_hip_rs_sharded_plan) over MPI
+ * point-to-point: MPI_Isend / MPI_Irecv of every message of an exchange,
+ * then MPI_Waitall -- the reference's own primitives (src/redset_reedsolomon.c:
+ * 690-694, :713-733) for builds without RCCL or across nodes. Buffers are
+ * host memory (device_buffers = 0), or device memory staged through pinned
+ * host buffers with hipMemcpyAsync (device_buffers = 1; no GPU-aware MPI
+ * needed). Messages above 1 GiB are split alike on both sides. */
+typedef struct redset_hip_mpi_transport redset_hip_mpi_transport;
+int redset_hip_mpi_transport_create(MPI_Comm comm, int device_buffers, redset_hip_transport* out,
+                                    redset_hip_mpi_transport** handle);
+void redset_hip_mpi_transport_destroy(redset_hip_mpi_transport* handle);
+
 #ifdef __cplusplus
 }
 #endif

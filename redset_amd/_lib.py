@@ -52,7 +52,20 @@ EXPORTED_SYMBOLS = (
     "redset_hip_hostio_destroy",
     "redset_hip_fileio_create",
     "redset_hip_fileio_destroy",
+    "redset_hip_shard_slice_bytes",
+    "redset_hip_rs_sharded_plan",
+    "redset_hip_sharded_execute",
+    "redset_hip_sharded_execute_phase",
+    "redset_hip_sharded_get_info",
+    "redset_hip_sharded_destroy",
+    "redset_hip_rccl_unique_id",
+    "redset_hip_rccl_transport_create",
+    "redset_hip_rccl_transport_destroy",
 )
+
+PHASE_GATHER = 0
+PHASE_COMPUTE = 1
+PHASE_RETURN = 2
 
 
 class RedsetHipUnavailable(RuntimeError):
@@ -98,6 +111,62 @@ class StreamStats(ctypes.Structure):
         return {k: getattr(self, k) for k, _ in self._fields_}
 
 
+class Xfer(ctypes.Structure):
+    """redset_hip_xfer: one message (or half of a local copy) of an exchange."""
+
+    _fields_ = [("peer", c_int), ("send", c_int), ("buf", c_void_p), ("len", c_size_t)]
+
+
+EXCHANGE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(Xfer), c_int, c_void_p)
+COMPUTE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, c_int, POINTER(c_int), POINTER(c_void_p), POINTER(c_void_p),
+                              c_size_t, c_size_t, c_void_p)
+
+
+class Transport(ctypes.Structure):
+    _fields_ = [("world", c_int), ("rank", c_int), ("exchange", c_void_p), ("ctx", c_void_p)]
+
+
+class Compute(ctypes.Structure):
+    _fields_ = [("run", c_void_p), ("ctx", c_void_p)]
+
+
+class ShardLayout(ctypes.Structure):
+    _fields_ = [
+        ("nsets", c_int),
+        ("host", POINTER(c_int)),
+        ("slot", POINTER(c_int)),
+        ("max_hosted", c_int),
+        ("chunk_size", c_size_t),
+        ("slice_bytes", c_size_t),
+        ("hosted_data", c_void_p),
+        ("hosted_parity", c_void_p),
+        ("gathered_data", c_void_p),
+        ("gathered_parity", c_void_p),
+    ]
+
+
+class ShardedInfo(ctypes.Structure):
+    _fields_ = [
+        ("kind", c_int),
+        ("world", c_int),
+        ("rank", c_int),
+        ("nsets", c_int),
+        ("missing", c_int),
+        ("my_slice_len", c_size_t),
+        ("gather_messages", c_int),
+        ("return_messages", c_int),
+        ("gather_bytes_sent", c_ulonglong),
+        ("gather_bytes_recv", c_ulonglong),
+        ("return_bytes_sent", c_ulonglong),
+        ("return_bytes_recv", c_ulonglong),
+        ("local_bytes", c_ulonglong),
+        ("compute_bytes", c_ulonglong),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
 _PP = POINTER(c_void_p)
 _IOP = POINTER(StreamIO)
 _STP = POINTER(StreamStats)
@@ -135,6 +204,17 @@ _SIGNATURES = {
          c_size_t, POINTER(c_int), _IOP, POINTER(c_void_p)],
     ),
     "redset_hip_fileio_destroy": (None, [c_void_p]),
+    "redset_hip_shard_slice_bytes": (c_size_t, [c_size_t, c_int]),
+    "redset_hip_rs_sharded_plan": (
+        c_int, [c_void_p, c_int, c_int, POINTER(c_int), POINTER(ShardLayout), POINTER(Transport), POINTER(Compute),
+                POINTER(c_void_p)]),
+    "redset_hip_sharded_execute": (c_int, [c_void_p, c_void_p]),
+    "redset_hip_sharded_execute_phase": (c_int, [c_void_p, c_int, c_void_p]),
+    "redset_hip_sharded_get_info": (c_int, [c_void_p, POINTER(ShardedInfo)]),
+    "redset_hip_sharded_destroy": (None, [c_void_p]),
+    "redset_hip_rccl_unique_id": (c_int, [POINTER(c_ubyte)]),
+    "redset_hip_rccl_transport_create": (c_int, [POINTER(c_ubyte), c_int, c_int, POINTER(Transport), POINTER(c_void_p)]),
+    "redset_hip_rccl_transport_destroy": (None, [c_void_p]),
     "redset_hip_last_error": (c_char_p, []),
     "redset_hip_record_error": (c_int, [c_char_p]),
     "redset_hip_version": (c_char_p, []),

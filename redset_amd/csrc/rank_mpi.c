@@ -554,3 +554,122 @@ out:
   free(req);
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
 }
+
+/* ---- MPI transport of the sharded path (include/redset_hip_mpi.h) ------- */
+
+#define MPI_PIECE ((size_t) 1 << 30) /* bytes per MPI message (int counts) */
+
+struct redset_hip_mpi_transport {
+  MPI_Comm comm;
+  int world, rank, device;
+  uint8_t* stage;   /* pinned staging (device mode) */
+  size_t stage_len;
+  MPI_Request* req;
+  int req_cap;
+};
+
+static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream) {
+  struct redset_hip_mpi_transport* T = (struct redset_hip_mpi_transport*) ctx;
+  hipStream_t s = (hipStream_t) stream;
+  size_t need = 0, nreq = 0;
+  for (int i = 0; i < n; ++i)
+    if (x[i].peer != T->rank) {
+      need += x[i].len;
+      nreq += (x[i].len + MPI_PIECE - 1) / MPI_PIECE;
+    }
+  if (T->device) {
+    if (need > T->stage_len) {
+      if (T->stage) (void) hipHostFree(T->stage);
+      T->stage = NULL;
+      T->stage_len = 0;
+      if (hipHostMalloc((void**) &T->stage, need, hipHostMallocDefault) != hipSuccess)
+        return fail("mpi transport: hipHostMalloc(%zu) failed", need);
+      T->stage_len = need;
+    }
+    /* work already on the stream produced the send buffers */
+    if (hipStreamSynchronize(s) != hipSuccess) return fail("mpi transport: stream sync failed");
+  }
+  if ((int) nreq > T->req_cap) {
+    MPI_Request* r = realloc(T->req, sizeof(*r) * nreq);
+    if (!r) return fail("out of host memory");
+    T->req = r;
+    T->req_cap = (int) nreq;
+  }
+  /* local copies, and (device mode) every send staged to host */
+  size_t off = 0;
+  for (int i = 0; i < n; ++i) {
+    if (x[i].peer == T->rank) {
+      if (i + 1 >= n || !x[i].send || x[i + 1].send || x[i + 1].peer != T->rank || x[i + 1].len != x[i].len)
+        return fail("mpi transport: malformed local copy");
+      if (T->device) {
+        if (hipMemcpyAsync(x[i + 1].buf, x[i].buf, x[i].len, hipMemcpyDeviceToDevice, s) != hipSuccess)
+          return fail("mpi transport: local copy failed");
+      } else {
+        memmove(x[i + 1].buf, x[i].buf, x[i].len);
+      }
+      ++i;
+      continue;
+    }
+    if (T->device && x[i].send &&
+        hipMemcpyAsync(T->stage + off, x[i].buf, x[i].len, hipMemcpyDeviceToHost, s) != hipSuccess)
+      return fail("mpi transport: D2H staging failed");
+    off += x[i].len;
+  }
+  if (T->device && hipStreamSynchronize(s) != hipSuccess) return fail("mpi transport: stream sync failed");
+  int k = 0;
+  off = 0;
+  for (int i = 0; i < n; ++i) {
+    if (x[i].peer == T->rank) {
+      ++i;
+      continue;
+    }
+    uint8_t* base = T->device ? T->stage + off : (uint8_t*) x[i].buf;
+    for (size_t done = 0; done < x[i].len; done += MPI_PIECE) {
+      const int cnt = (int) min_sz(MPI_PIECE, x[i].len - done);
+      if (x[i].send) MPI_Isend(base + done, cnt, MPI_BYTE, x[i].peer, 7, T->comm, &T->req[k++]);
+      else MPI_Irecv(base + done, cnt, MPI_BYTE, x[i].peer, 7, T->comm, &T->req[k++]);
+    }
+    off += x[i].len;
+  }
+  if (MPI_Waitall(k, T->req, MPI_STATUSES_IGNORE) != MPI_SUCCESS) return fail("mpi transport: MPI_Waitall failed");
+  if (!T->device) return 0;
+  off = 0;
+  for (int i = 0; i < n; ++i) {
+    if (x[i].peer == T->rank) {
+      ++i;
+      continue;
+    }
+    if (!x[i].send && hipMemcpyAsync(x[i].buf, T->stage + off, x[i].len, hipMemcpyHostToDevice, s) != hipSuccess)
+      return fail("mpi transport: H2D failed");
+    off += x[i].len;
+  }
+  /* the staging buffer is reused by the next exchange */
+  return hipStreamSynchronize(s) == hipSuccess ? 0 : fail("mpi transport: stream sync failed");
+}
+
+int redset_hip_mpi_transport_create(MPI_Comm comm, int device_buffers, redset_hip_transport* out,
+                                    redset_hip_mpi_transport** handle) {
+  if (!out || !handle) return fail("mpi_transport_create: null argument");
+  *handle = NULL;
+  struct redset_hip_mpi_transport* T = calloc(1, sizeof(*T));
+  if (!T) return fail("out of host memory");
+  if (comm_geometry(comm, &T->world, &T->rank)) {
+    free(T);
+    return REDSET_FAILURE;
+  }
+  T->comm = comm;
+  T->device = device_buffers != 0;
+  out->world = T->world;
+  out->rank = T->rank;
+  out->exchange = mpi_exchange;
+  out->ctx = T;
+  *handle = T;
+  return REDSET_SUCCESS;
+}
+
+void redset_hip_mpi_transport_destroy(redset_hip_mpi_transport* T) {
+  if (!T) return;
+  if (T->stage) (void) hipHostFree(T->stage);
+  free(T->req);
+  free(T);
+}

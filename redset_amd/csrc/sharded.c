@@ -1,0 +1,427 @@
+/*
+ * sharded.c -- sets sharded over the GPUs of a node (include/redset_hip.h,
+ * "sets sharded over the GPUs of a node"). Host code in C over the codec's
+ * own C ABI; the exchanges go through a caller-chosen transport (RCCL over
+ * xGMI in production, transport_rccl.c; MPI host buffers, rank_mpi.c; a test
+ * callback) and the arithmetic through the HIP plans or a compute callback.
+ *
+ * Replaces, for the multi-rank rebuild, the decode ring of
+ * redset_reedsolomon_decode (src/redset_reedsolomon.c:646-703: p-1 steps,
+ * one cell per step per rank) with one grouped gather of column slices, and
+ * its gather of solved cells to the failed ranks (:713-733) with one grouped
+ * return; for encode, the ring of redset_reedsolomon_encode (:329-377).
+ * Stripe ownership differs on purpose: the reference has rank r solve stripe
+ * r whole (:606-611); here every GPU solves its column slice of every stripe,
+ * so the work splits evenly whatever p and the number of GPUs.
+ */
+#include <stdarg.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "redset_hip.h"
+
+#define MAX_RANKS 256
+
+static int sfail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
+static int sfail(const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  return redset_hip_record_error(buf);
+}
+
+/* ---- transfer lists ---------------------------------------------------- */
+
+typedef struct {
+  redset_hip_xfer* v;
+  int n, cap;
+} xlist;
+
+static int xl_push(xlist* L, redset_hip_xfer x) {
+  if (L->n == L->cap) {
+    int cap = L->cap ? 2 * L->cap : 64;
+    redset_hip_xfer* v = realloc(L->v, sizeof(*v) * (size_t) cap);
+    if (!v) return sfail("out of host memory");
+    L->v = v;
+    L->cap = cap;
+  }
+  L->v[L->n++] = x;
+  return 0;
+}
+
+/* Per-peer message lists of one exchange. Rows appended to a peer's send (or
+ * receive) list merge with the previous one when contiguous in local memory.
+ * Both processes of a pair walk the same rows in the same order, and a row's
+ * offset on one side differs from its offset on the other by a constant of
+ * the pair (the buffers share one layout), so they merge alike and the
+ * message lengths match. Local copies keep (src, dst) pairs. */
+typedef struct {
+  int world, rank;
+  xlist* send;   /* [world] */
+  xlist* recv;   /* [world] */
+  xlist copy;    /* src, dst, src, dst, ... */
+} exch;
+
+static int ex_init(exch* X, int world, int rank) {
+  memset(X, 0, sizeof(*X));
+  X->world = world;
+  X->rank = rank;
+  X->send = calloc((size_t) world, sizeof(xlist));
+  X->recv = calloc((size_t) world, sizeof(xlist));
+  return (X->send && X->recv) ? 0 : sfail("out of host memory");
+}
+
+static void ex_free(exch* X) {
+  for (int g = 0; X->send && g < X->world; ++g) free(X->send[g].v);
+  for (int g = 0; X->recv && g < X->world; ++g) free(X->recv[g].v);
+  free(X->send);
+  free(X->recv);
+  free(X->copy.v);
+  memset(X, 0, sizeof(*X));
+}
+
+static int ex_row(xlist* L, int peer, int send, unsigned char* buf, size_t len) {
+  if (L->n > 0) {
+    redset_hip_xfer* t = &L->v[L->n - 1];
+    if ((unsigned char*) t->buf + t->len == buf) {
+      t->len += len;
+      return 0;
+    }
+  }
+  redset_hip_xfer x = {peer, send, buf, len};
+  return xl_push(L, x);
+}
+
+static int ex_send(exch* X, int peer, unsigned char* buf, size_t len) { return ex_row(&X->send[peer], peer, 1, buf, len); }
+static int ex_recv(exch* X, int peer, unsigned char* buf, size_t len) { return ex_row(&X->recv[peer], peer, 0, buf, len); }
+
+static int ex_copy(exch* X, unsigned char* dst, const unsigned char* src, size_t len) {
+  xlist* L = &X->copy;
+  if (L->n >= 2) {
+    redset_hip_xfer* s = &L->v[L->n - 2];
+    redset_hip_xfer* d = &L->v[L->n - 1];
+    if ((const unsigned char*) s->buf + s->len == src && (unsigned char*) d->buf + d->len == dst) {
+      s->len += len;
+      d->len += len;
+      return 0;
+    }
+  }
+  redset_hip_xfer a = {X->rank, 1, (void*) src, len};
+  redset_hip_xfer b = {X->rank, 0, dst, len};
+  int rc = xl_push(L, a);
+  return rc ? rc : xl_push(L, b);
+}
+
+/* flatten into one list for the transport: local copies, then per peer its
+ * sends and receives; byte counts for the info block */
+static int ex_flatten(exch* X, xlist* out, int* messages, unsigned long long* sent, unsigned long long* recvd,
+                      unsigned long long* local) {
+  for (int i = 0; i < X->copy.n; ++i) {
+    if (xl_push(out, X->copy.v[i])) return REDSET_FAILURE;
+    if (X->copy.v[i].send) *local += X->copy.v[i].len;
+  }
+  for (int g = 0; g < X->world; ++g) {
+    for (int i = 0; i < X->send[g].n; ++i) {
+      if (xl_push(out, X->send[g].v[i])) return REDSET_FAILURE;
+      *sent += X->send[g].v[i].len;
+      ++*messages;
+    }
+    for (int i = 0; i < X->recv[g].n; ++i) {
+      if (xl_push(out, X->recv[g].v[i])) return REDSET_FAILURE;
+      *recvd += X->recv[g].v[i].len;
+    }
+  }
+  return 0;
+}
+
+/* ---- the plan ---------------------------------------------------------- */
+
+struct redset_hip_sharded {
+  redset_hip_sharded_info info;
+  redset_hip_transport tr;
+  redset_hip_compute comp;
+  int p, e, missing;
+  int lost[MAX_RANKS];
+  size_t W;
+  xlist gather, ret;
+  /* compute per set: HIP plans, or the member pointers for the callback */
+  redset_hip_plan** plans;         /* [nsets] (NULL entries when my slice is empty) */
+  unsigned char** lofi;            /* [nsets * p] */
+  unsigned char** parity;          /* [nsets * p] */
+};
+
+size_t redset_hip_shard_slice_bytes(size_t chunk_size, int world) {
+  if (world < 1) world = 1;
+  size_t w = (chunk_size + (size_t) world - 1) / (size_t) world;
+  return (w + 255) & ~(size_t) 255;
+}
+
+/* Which cells of each member some stripe's decode reads: need[r*p + c] for
+ * member r's cell in stripe c (data or parity, whichever it is). Encode
+ * reads every data cell. */
+static int plan_inputs(const redset_hip_rs* rs, int p, int e, int kind, int missing, const int* lost,
+                       unsigned char* need) {
+  memset(need, 0, (size_t) p * p);
+  if (kind == REDSET_HIP_PLAN_RS_ENCODE) {
+    for (int r = 0; r < p; ++r)
+      for (int c = 0; c < p; ++c) need[r * p + c] = redset_hip_rs_get_encoding_id(p, e, r, c) < p;
+    return 0;
+  }
+  unsigned char* D = malloc((size_t) missing * p);
+  if (!D) return sfail("out of host memory");
+  for (int c = 0; c < p; ++c) {
+    if (redset_hip_rs_decode_matrix(rs, missing, lost, c, D)) {
+      free(D);
+      return REDSET_FAILURE;
+    }
+    for (int r = 0; r < p; ++r)
+      for (int i = 0; i < missing; ++i)
+        if (D[(size_t) i * p + r]) need[r * p + c] = 1;
+  }
+  free(D);
+  return 0;
+}
+
+/* member r's cell in stripe c: data cell index, or -(1 + parity slot) */
+static int cell_of(int p, int e, int r, int c) {
+  const int enc = redset_hip_rs_get_encoding_id(p, e, r, c);
+  return enc < p ? redset_hip_rs_get_data_id(p, e, r, c) : -(1 + (enc - p));
+}
+
+int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
+                               const redset_hip_shard_layout* L, const redset_hip_transport* tr,
+                               const redset_hip_compute* comp, redset_hip_sharded** out) {
+  int p, e;
+  if (!out) return sfail("sharded_plan: null out-pointer");
+  *out = NULL;
+  if (!rs || !L || !tr || !tr->exchange) return sfail("sharded_plan: null argument");
+  if (redset_hip_rs_shape(rs, &p, &e)) return REDSET_FAILURE;
+  if (kind != REDSET_HIP_PLAN_RS_ENCODE && kind != REDSET_HIP_PLAN_RS_REBUILD)
+    return sfail("sharded_plan: kind %d is not RS encode or rebuild", kind);
+  if (kind == REDSET_HIP_PLAN_RS_ENCODE) missing = 0;
+  if (kind == REDSET_HIP_PLAN_RS_REBUILD) {
+    if (missing < 1 || missing > e) return sfail("cannot rebuild %d members with %d parity chunks", missing, e);
+    if (!rebuild_ranks) return sfail("null rebuild_ranks");
+    for (int i = 0; i < missing; ++i)
+      if (rebuild_ranks[i] < 0 || rebuild_ranks[i] >= p || (i && rebuild_ranks[i] <= rebuild_ranks[i - 1]))
+        return sfail("rebuild ranks must be ascending members of 0..%d", p - 1);
+  }
+  const int world = tr->world, me = tr->rank, d = p - e;
+  if (world < 1 || me < 0 || me >= world) return sfail("transport world %d / rank %d invalid", world, me);
+  if (L->nsets < 1 || !L->host || !L->slot || L->max_hosted < 1) return sfail("sharded layout: bad placement");
+  const size_t W = L->slice_bytes;
+  if (W == 0 || W * (size_t) world < L->chunk_size) return sfail("slice_bytes %zu too small for %zu over %d", W,
+                                                                   L->chunk_size, world);
+  if (!L->hosted_data || !L->hosted_parity || !L->gathered_data || !L->gathered_parity)
+    return sfail("sharded layout: null buffer");
+  const int nm = L->nsets * p, mh = L->max_hosted;
+  {
+    /* every (host, slot) at most once */
+    unsigned char* used = calloc((size_t) world * mh, 1);
+    if (!used) return sfail("out of host memory");
+    for (int m = 0; m < nm; ++m) {
+      const int h = L->host[m], j = L->slot[m];
+      if (h < 0 || h >= world || j < 0 || j >= mh || used[(size_t) h * mh + j]) {
+        free(used);
+        return sfail("sharded layout: member %d placed at (%d, %d) invalid or twice", m, h, j);
+      }
+      used[(size_t) h * mh + j] = 1;
+    }
+    free(used);
+  }
+
+  redset_hip_sharded* P = calloc(1, sizeof(*P));
+  unsigned char* need = malloc((size_t) p * p);
+  int* by_slot = malloc(sizeof(int) * (size_t) world * mh); /* (h, j) -> member, or -1 */
+  exch G, R;
+  memset(&G, 0, sizeof(G));
+  memset(&R, 0, sizeof(R));
+  int rc = (!P || !need || !by_slot) ? sfail("out of host memory") : 0;
+  if (!rc) rc = ex_init(&G, world, me);
+  if (!rc) rc = ex_init(&R, world, me);
+  if (rc) goto done;
+  P->tr = *tr;
+  if (comp) P->comp = *comp;
+  P->p = p;
+  P->e = e;
+  P->missing = missing;
+  for (int i = 0; i < missing; ++i) P->lost[i] = rebuild_ranks[i];
+  P->W = W;
+  P->info.kind = kind;
+  P->info.world = world;
+  P->info.rank = me;
+  P->info.nsets = L->nsets;
+  P->info.missing = missing;
+  {
+    const size_t lo = (size_t) me * W;
+    P->info.my_slice_len = lo >= L->chunk_size ? 0 : (L->chunk_size - lo < W ? L->chunk_size - lo : W);
+  }
+  for (int i = 0; i < world * mh; ++i) by_slot[i] = -1;
+  for (int m = 0; m < nm; ++m) by_slot[(size_t) L->host[m] * mh + L->slot[m]] = m;
+  if ((rc = plan_inputs(rs, p, e, kind, missing, rebuild_ranks, need))) goto done;
+
+  /* addresses in this process's buffers */
+#define HD(q, j, s) (L->hosted_data + ((((size_t) (q) * mh + (j)) * d + (s)) * W))
+#define HP(q, j, i) (L->hosted_parity + ((((size_t) (q) * mh + (j)) * e + (i)) * W))
+#define GD(h, j, s) (L->gathered_data + ((((size_t) (h) * mh + (j)) * d + (s)) * W))
+#define GP(h, j, i) (L->gathered_parity + ((((size_t) (h) * mh + (j)) * e + (i)) * W))
+
+  /* gather: slice g of every needed cell of every surviving member goes from
+   * its host to process g; data rows then parity rows, members in slot order */
+  for (int g = 0; g < world && !rc; ++g) {
+    for (int pass = 0; pass < 2 && !rc; ++pass) {
+      const int ncell = pass == 0 ? d : e;
+      /* what I send to g (g == me: copy) */
+      for (int j = 0; j < mh && !rc; ++j) {
+        const int m = by_slot[(size_t) me * mh + j];
+        if (m < 0) continue;
+        const int r = m % p;
+        for (int x = 0; x < ncell && !rc; ++x) {
+          int wanted = 0;
+          for (int c = 0; c < p && !wanted; ++c)
+            if (need[r * p + c] && cell_of(p, e, r, c) == (pass == 0 ? x : -(1 + x))) wanted = 1;
+          if (!wanted) continue;
+          unsigned char* src = pass == 0 ? HD(g, j, x) : HP(g, j, x);
+          if (g == me) rc = ex_copy(&G, pass == 0 ? GD(me, j, x) : GP(me, j, x), src, W);
+          else rc = ex_send(&G, g, src, W);
+        }
+      }
+      if (g == me) continue;
+      /* what I receive from g: my slice of g's members' needed cells */
+      for (int j = 0; j < mh && !rc; ++j) {
+        const int m = by_slot[(size_t) g * mh + j];
+        if (m < 0) continue;
+        const int r = m % p;
+        for (int x = 0; x < ncell && !rc; ++x) {
+          int wanted = 0;
+          for (int c = 0; c < p && !wanted; ++c)
+            if (need[r * p + c] && cell_of(p, e, r, c) == (pass == 0 ? x : -(1 + x))) wanted = 1;
+          if (wanted) rc = ex_recv(&G, g, pass == 0 ? GD(g, j, x) : GP(g, j, x), W);
+        }
+      }
+    }
+  }
+
+  /* return: the outputs (encode: every member's parity; rebuild: every cell
+   * of the lost members) go from each process's gathered slots to the
+   * member's host: data rows, then parity rows, members in set order */
+  for (int pass = 0; pass < 2 && !rc; ++pass) {
+    if (pass == 0 && kind == REDSET_HIP_PLAN_RS_ENCODE) continue; /* encode returns parity only */
+    for (int m = 0; m < nm && !rc; ++m) {
+      const int r = m % p;
+      int is_out = kind == REDSET_HIP_PLAN_RS_ENCODE;
+      for (int i = 0; i < missing; ++i) is_out |= P->lost[i] == r;
+      if (!is_out) continue;
+      const int h = L->host[m], j = L->slot[m];
+      const size_t len = (size_t) (pass == 0 ? d : e) * W;
+      unsigned char* mine = pass == 0 ? GD(h, j, 0) : GP(h, j, 0);
+      if (h != me) {
+        rc = ex_send(&R, h, mine, len);
+        continue;
+      }
+      for (int g = 0; g < world && !rc; ++g) {
+        unsigned char* dst = pass == 0 ? HD(g, j, 0) : HP(g, j, 0);
+        rc = g == me ? ex_copy(&R, dst, mine, len) : ex_recv(&R, g, dst, len);
+      }
+    }
+  }
+  if (!rc) rc = ex_flatten(&G, &P->gather, &P->info.gather_messages, &P->info.gather_bytes_sent,
+                           &P->info.gather_bytes_recv, &P->info.local_bytes);
+  if (!rc) rc = ex_flatten(&R, &P->ret, &P->info.return_messages, &P->info.return_bytes_sent,
+                           &P->info.return_bytes_recv, &P->info.local_bytes);
+  if (rc) goto done;
+
+  /* compute: every set over my slices in the gathered layout (cell stride W) */
+  P->plans = calloc((size_t) L->nsets, sizeof(*P->plans));
+  P->lofi = malloc(sizeof(*P->lofi) * (size_t) nm);
+  P->parity = malloc(sizeof(*P->parity) * (size_t) nm);
+  if (!P->plans || !P->lofi || !P->parity) {
+    rc = sfail("out of host memory");
+    goto done;
+  }
+  for (int m = 0; m < nm; ++m) {
+    P->lofi[m] = GD(L->host[m], L->slot[m], 0);
+    P->parity[m] = GP(L->host[m], L->slot[m], 0);
+  }
+  const size_t n = P->info.my_slice_len;
+  P->info.compute_bytes = (unsigned long long) L->nsets * p * (d + (kind == REDSET_HIP_PLAN_RS_ENCODE ? e : missing)) * n;
+  for (int k = 0; k < L->nsets && !rc && n > 0 && !P->comp.run; ++k) {
+    unsigned char* const* lf = P->lofi + (size_t) k * p;
+    unsigned char* const* pr = P->parity + (size_t) k * p;
+    rc = kind == REDSET_HIP_PLAN_RS_ENCODE ? redset_hip_rs_plan_encode(rs, lf, pr, n, W, &P->plans[k])
+                                           : redset_hip_rs_plan_rebuild(rs, missing, P->lost, lf, pr, n, W, &P->plans[k]);
+  }
+#undef HD
+#undef HP
+#undef GD
+#undef GP
+
+done:
+  ex_free(&G);
+  ex_free(&R);
+  free(need);
+  free(by_slot);
+  if (rc) {
+    redset_hip_sharded_destroy(P);
+    return REDSET_FAILURE;
+  }
+  *out = P;
+  return REDSET_SUCCESS;
+}
+
+int redset_hip_sharded_execute_phase(redset_hip_sharded* P, int phase, void* stream) {
+  if (!P) return sfail("null sharded plan");
+  switch (phase) {
+    case REDSET_HIP_PHASE_GATHER:
+      if (P->gather.n && P->tr.exchange(P->tr.ctx, P->gather.v, P->gather.n, stream) != 0)
+        return sfail("sharded gather: transport exchange failed");
+      return REDSET_SUCCESS;
+    case REDSET_HIP_PHASE_COMPUTE: {
+      const size_t n = P->info.my_slice_len;
+      if (n == 0) return REDSET_SUCCESS;
+      for (int k = 0; k < P->info.nsets; ++k) {
+        if (P->comp.run) {
+          if (P->comp.run(P->comp.ctx, P->info.kind, P->missing, P->lost, P->lofi + (size_t) k * P->p,
+                          P->parity + (size_t) k * P->p, n, P->W, stream) != 0)
+            return sfail("sharded compute callback failed (set %d)", k);
+        } else if (redset_hip_plan_execute(P->plans[k], stream)) {
+          return REDSET_FAILURE;
+        }
+      }
+      return REDSET_SUCCESS;
+    }
+    case REDSET_HIP_PHASE_RETURN:
+      if (P->ret.n && P->tr.exchange(P->tr.ctx, P->ret.v, P->ret.n, stream) != 0)
+        return sfail("sharded return: transport exchange failed");
+      return REDSET_SUCCESS;
+    default:
+      return sfail("unknown sharded phase %d", phase);
+  }
+}
+
+int redset_hip_sharded_execute(redset_hip_sharded* P, void* stream) {
+  for (int ph = REDSET_HIP_PHASE_GATHER; ph <= REDSET_HIP_PHASE_RETURN; ++ph)
+    if (redset_hip_sharded_execute_phase(P, ph, stream)) return REDSET_FAILURE;
+  return REDSET_SUCCESS;
+}
+
+int redset_hip_sharded_get_info(const redset_hip_sharded* P, redset_hip_sharded_info* info) {
+  if (!P || !info) return sfail("null argument");
+  *info = P->info;
+  return REDSET_SUCCESS;
+}
+
+void redset_hip_sharded_destroy(redset_hip_sharded* P) {
+  if (!P) return;
+  for (int k = 0; P->plans && k < P->info.nsets; ++k) redset_hip_plan_destroy(P->plans[k]);
+  free(P->plans);
+  free(P->lofi);
+  free(P->parity);
+  free(P->gather.v);
+  free(P->ret.v);
+  free(P);
+}

@@ -1,0 +1,93 @@
+/*
+ * transport_rccl.c -- the sharded path's transport over RCCL / xGMI
+ * (include/redset_hip.h: redset_hip_rccl_*). One exchange = one
+ * ncclGroupStart/End of point-to-point ncclSend / ncclRecv on the caller's
+ * stream (RCCL schedules them over the xGMI links), local copies as
+ * hipMemcpyAsync on the same stream. This is what replaces the reference's
+ * MPI_Irecv / MPI_Isend ring and gather (src/redset_reedsolomon.c:690-694,
+ * :713-733) for the multi-rank rebuild.
+ */
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "redset_hip.h"
+
+struct redset_hip_rccl {
+  ncclComm_t comm;
+  int world, rank;
+};
+
+static int rfail(const char* what, ncclResult_t r) {
+  char buf[256];
+  snprintf(buf, sizeof(buf), "%s: %s", what, ncclGetErrorString(r));
+  return redset_hip_record_error(buf);
+}
+
+static int rccl_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream) {
+  struct redset_hip_rccl* R = (struct redset_hip_rccl*) ctx;
+  hipStream_t s = (hipStream_t) stream;
+  for (int i = 0; i < n; ++i) {
+    if (x[i].peer != R->rank) continue;
+    /* local copy: the send entry (source) is followed by its receive (destination) */
+    if (!x[i].send || i + 1 >= n || x[i + 1].peer != R->rank || x[i + 1].send || x[i + 1].len != x[i].len)
+      return redset_hip_record_error("rccl exchange: malformed local copy");
+    if (hipMemcpyAsync(x[i + 1].buf, x[i].buf, x[i].len, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      return redset_hip_record_error("rccl exchange: local hipMemcpyAsync failed");
+    ++i;
+  }
+  ncclResult_t r = ncclGroupStart();
+  if (r != ncclSuccess) return rfail("ncclGroupStart", r);
+  for (int i = 0; i < n; ++i) {
+    if (x[i].peer == R->rank) continue;
+    r = x[i].send ? ncclSend(x[i].buf, x[i].len, ncclUint8, x[i].peer, R->comm, s)
+                  : ncclRecv(x[i].buf, x[i].len, ncclUint8, x[i].peer, R->comm, s);
+    if (r != ncclSuccess) {
+      (void) ncclGroupEnd();
+      return rfail(x[i].send ? "ncclSend" : "ncclRecv", r);
+    }
+  }
+  r = ncclGroupEnd();
+  return r == ncclSuccess ? 0 : rfail("ncclGroupEnd", r);
+}
+
+int redset_hip_rccl_unique_id(unsigned char id_out[128]) {
+  ncclUniqueId id;
+  if (!id_out) return redset_hip_record_error("rccl_unique_id: null argument");
+  ncclResult_t r = ncclGetUniqueId(&id);
+  if (r != ncclSuccess) return rfail("ncclGetUniqueId", r);
+  memcpy(id_out, &id, sizeof(id) < 128 ? sizeof(id) : 128);
+  return REDSET_SUCCESS;
+}
+
+int redset_hip_rccl_transport_create(const unsigned char id[128], int world, int rank, redset_hip_transport* out,
+                                     redset_hip_rccl** handle) {
+  if (!id || !out || !handle) return redset_hip_record_error("rccl_transport_create: null argument");
+  *handle = NULL;
+  if (world < 1 || rank < 0 || rank >= world) return redset_hip_record_error("rccl_transport_create: bad world/rank");
+  struct redset_hip_rccl* R = calloc(1, sizeof(*R));
+  if (!R) return redset_hip_record_error("out of host memory");
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid) < 128 ? sizeof(uid) : 128);
+  ncclResult_t r = ncclCommInitRank(&R->comm, world, uid, rank);
+  if (r != ncclSuccess) {
+    free(R);
+    return rfail("ncclCommInitRank", r);
+  }
+  R->world = world;
+  R->rank = rank;
+  out->world = world;
+  out->rank = rank;
+  out->exchange = rccl_exchange;
+  out->ctx = R;
+  *handle = R;
+  return REDSET_SUCCESS;
+}
+
+void redset_hip_rccl_transport_destroy(redset_hip_rccl* R) {
+  if (!R) return;
+  (void) ncclCommDestroy(R->comm);
+  free(R);
+}

@@ -1,79 +1,53 @@
 """Multi-GPU encode / rebuild of redundancy sets spread over the GPUs of a node.
 
-Replaces the reference's MPI rings (encode: src/redset_reedsolomon.c:346-363;
-decode reduce + gather: :690-733) with one all-to-all gather of cell column
-slices over RCCL/xGMI, a local gf_mac pass on each GPU's column slice of
-every stripe, and one exchange that returns the result slices to their owners.
+A thin Python face of the C ABI's sharded path (include/redset_hip.h, "sets
+sharded over the GPUs of a node"; redset_amd/csrc/sharded.c): the C library
+plans which column slices go where, runs the exchanges through a transport
+and the gf_mac kernel on this GPU's slice of every stripe. This module only
+chooses the placement, allocates the slabs (torch tensors in HBM) and picks
+the transport: RCCL over xGMI (redset_hip_rccl_*, the production path), or,
+for CPU tests, a callback transport over torch.distributed (gloo).
+
+Replaces the reference's MPI rings (encode: src/redset_reedsolomon.c:329-377;
+decode reduce + gather: :646-733) with one grouped gather of cell column
+slices, a local gf_mac pass, and one grouped return.
 
 World layout (weak scaling): ``world`` sets of ``p`` members; member m of the
 world (set m // p, index m % p) lives on GPU m % world, so every GPU hosts p
-members and a set's members spread over the GPUs. Every cell is cut into
-``world`` column slices of ``W`` bytes; GPU g computes slice g of every stripe
-of every set. Byte j of a parity/rebuilt cell depends only on byte j of its
-stripe's inputs, so the slices are independent.
+members and a set's members spread over the GPUs. Each GPU lists its hosted
+members with the lost ones last. Every cell is cut into ``world`` column
+slices of ``W`` bytes; GPU g computes slice g of every stripe of every set.
 
-HBM layout per GPU (so each exchange is one contiguous all-to-all):
-  hosted data   D_host[g][j][s][W]  slice g of data cell s of hosted member j
-  hosted parity P_host[g][j][i][W]  slice g of parity cell i of hosted member j
+HBM layout per GPU (include/redset_hip.h):
+  hosted data   D_host[q][j][s][W]  slice q of data cell s of hosted member j
+  hosted parity P_host[q][j][i][W]  slice q of parity cell i of hosted member j
   gathered      D_gath[h][j][s][W]  my slice of data cell s of member j hosted on h
                 P_gath[h][j][i][W]  my slice of parity cell i of that member
-A member's logical file is therefore stored as `world` column slabs; the
-single-GPU path (bench N=1) keeps cells contiguous.
-
-The compute backend is pluggable so the exchange logic can be tested with
-gloo on CPU (tests/test_dist.py injects a CPU checker backend); the default
-backend is the HIP library.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
-from typing import Callable, Dict, List, Sequence, Tuple
+import ctypes
+from ctypes import c_int, c_ubyte, c_void_p
+from typing import List, Optional, Sequence, Tuple
 
 import numpy as np
 import torch
 import torch.distributed as dist
 
-SLICE_ALIGN = 256
-
-
-@dataclass
-class SetViews:
-    """Per-member base tensors of one set in a gathered layout (stride W)."""
-
-    lofi: List[torch.Tensor]    # member r: d cells of W bytes, contiguous
-    parity: List[torch.Tensor]  # member r: e cells of W bytes
-
-
-class HipBackend:
-    """Default compute: the HIP plans of redset_amd (gf_mac kernel)."""
-
-    def __init__(self, p: int, e: int):
-        from . import codec
-
-        self.codec = codec.RSCodec(p, e)
-
-    def prepare_encode(self, views: SetViews, nbytes: int, stride: int) -> Callable[[], None]:
-        plan = self.codec.plan_encode([t.data_ptr() for t in views.lofi], [t.data_ptr() for t in views.parity],
-                                      nbytes, stride)
-        return lambda: plan.execute()
-
-    def prepare_rebuild(self, views: SetViews, lost: Sequence[int], nbytes: int, stride: int) -> Callable[[], None]:
-        plan = self.codec.plan_rebuild(list(lost), [t.data_ptr() for t in views.lofi],
-                                       [t.data_ptr() for t in views.parity], nbytes, stride)
-        return lambda: plan.execute()
+from . import _lib
 
 
 def rebuild_inputs(p: int, e: int, lost: Sequence[int]) -> Tuple[np.ndarray, np.ndarray]:
     """Which cells of each surviving member some stripe's decode reads.
 
-    Returns (data[p][d], parity[p][e]) boolean masks. A stripe's decode
+    Returns (data[p][d], parity[p][e]) boolean masks (a cross-check of the C
+    planner's gather, tests/test_dist.py). A stripe's decode
     (redset_rs_reduce_decode + redset_rs_gaussian_solve as one linear map,
     redset_hip_rs_decode_matrix) reads the stripe's surviving data cells and
     the parity rows redset_rs_gaussian_solve_identify_rows selects
-    (src/redset_reedsolomon_common.c:425-564); the parity rows it leaves out
-    never have to cross the fabric. Member s's cell in stripe c is data cell
-    get_data_id(s, c) when get_encoding_id(s, c) < p, else parity slot
-    get_encoding_id(s, c) - p (src/redset_reedsolomon_common.c:822-853)."""
+    (src/redset_reedsolomon_common.c:425-564). Member s's cell in stripe c is
+    data cell get_data_id(s, c) when get_encoding_id(s, c) < p, else parity
+    slot get_encoding_id(s, c) - p (src/redset_reedsolomon_common.c:822-853)."""
     from .codec import RSCodec
 
     d = p - e
@@ -96,55 +70,172 @@ def rebuild_inputs(p: int, e: int, lost: Sequence[int]) -> Tuple[np.ndarray, np.
     return need_d, need_p
 
 
-def _runs(flags: Sequence[bool]) -> List[Tuple[int, int]]:
-    """[a, b) index ranges of the True entries"""
-    out, a = [], None
-    for i, f in enumerate(list(flags) + [False]):
-        if f and a is None:
-            a = i
-        elif not f and a is not None:
-            out.append((a, i))
-            a = None
-    return out
+class _Buffers:
+    """Address -> tensor view over the runner's four slabs, for callbacks."""
+
+    def __init__(self, tensors):
+        self.spans = sorted((t.data_ptr(), t.data_ptr() + t.numel(), t.view(-1)) for t in tensors)
+
+    def view(self, addr: int, n: int) -> torch.Tensor:
+        for lo, hi, flat in self.spans:
+            if lo <= addr and addr + n <= hi:
+                return flat[addr - lo: addr - lo + n]
+        raise ValueError(f"address {addr:#x}+{n} is outside the sharded buffers")
+
+
+class TorchTransport:
+    """redset_hip_transport over torch.distributed point-to-point
+    (batch_isend_irecv): for gloo runs on CPU; the C planner is unchanged."""
+
+    def __init__(self, world: int, rank: int, bufs: _Buffers):
+        self.bufs = bufs
+        self._fn = _lib.EXCHANGE_FN(self._exchange)
+        self.struct = _lib.Transport(world, rank, ctypes.cast(self._fn, c_void_p), None)
+        self.rank = rank
+
+    def _exchange(self, ctx, xfers, n, stream) -> int:
+        try:
+            ops = []
+            i = 0
+            while i < n:
+                x = xfers[i]
+                if x.peer == self.rank:  # local copy: source, then destination
+                    y = xfers[i + 1]
+                    self.bufs.view(y.buf, y.len).copy_(self.bufs.view(x.buf, x.len))
+                    i += 2
+                    continue
+                t = self.bufs.view(x.buf, x.len)
+                ops.append(dist.P2POp(dist.isend if x.send else dist.irecv, t, x.peer))
+                i += 1
+            if ops:
+                for req in dist.batch_isend_irecv(ops):
+                    req.wait()
+            return 0
+        except Exception as exc:  # noqa: BLE001 -- reported through the C error path
+            _lib.load().redset_hip_record_error(f"torch transport: {exc}".encode())
+            return 1
+
+    def close(self):
+        pass
+
+
+class RcclTransport:
+    """redset_hip_rccl_*: grouped ncclSend / ncclRecv over xGMI. Rank 0's
+    unique id reaches the others through the torch process group (any
+    channel would do)."""
+
+    def __init__(self, world: int, rank: int):
+        L = _lib.load()
+        uid = (c_ubyte * 128)()
+        if rank == 0:
+            _lib.check(L.redset_hip_rccl_unique_id(uid), "rccl_unique_id")
+        if world > 1:
+            t = torch.tensor(list(bytes(uid)), dtype=torch.uint8,
+                             device="cuda" if dist.get_backend() == "nccl" else "cpu")
+            dist.broadcast(t, src=0)
+            uid = (c_ubyte * 128)(*t.cpu().tolist())
+        self.struct = _lib.Transport()
+        h = c_void_p()
+        _lib.check(L.redset_hip_rccl_transport_create(uid, world, rank, ctypes.byref(self.struct), ctypes.byref(h)),
+                   "rccl_transport_create")
+        self._h = h
+
+    def close(self):
+        if self._h:
+            _lib.load().redset_hip_rccl_transport_destroy(self._h)
+            self._h = None
+
+
+class CallbackCompute:
+    """redset_hip_compute over a Python backend with
+    ``run(kind, lost, lofi_views, parity_views, nbytes, stride)`` (tests put
+    the CPU oracle here)."""
+
+    def __init__(self, backend, p: int, bufs: _Buffers):
+        self.backend, self.p, self.bufs = backend, p, bufs
+        self._fn = _lib.COMPUTE_FN(self._run)
+        self.struct = _lib.Compute(ctypes.cast(self._fn, c_void_p), None)
+
+    def _run(self, ctx, kind, missing, ranks, lofi, parity, nbytes, stride, stream) -> int:
+        try:
+            lost = [ranks[i] for i in range(missing)]
+            lv = [lofi[r] for r in range(self.p)]
+            pv = [parity[r] for r in range(self.p)]
+            self.backend.run(kind, lost, lv, pv, nbytes, stride, self.bufs)
+            return 0
+        except Exception as exc:  # noqa: BLE001
+            _lib.load().redset_hip_record_error(f"compute callback: {exc}".encode())
+            return 1
 
 
 class ShardedSetRunner:
     """Encode + rebuild of `world` sets column-sharded over `world` ranks."""
 
     def __init__(self, p: int, e: int, chunk: int, lost: Sequence[int], world: int, rank: int,
-                 device=None, backend=None, seed: int = 1234, fill: bool = True):
+                 device=None, backend=None, seed: int = 1234, fill: bool = True, transport: Optional[str] = None):
         self.p, self.e, self.d = p, e, p - e
         self.chunk, self.world, self.rank = chunk, world, rank
         self.lost = sorted(lost)
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
-        W = -(-chunk // world)
-        self.W = -(-W // SLICE_ALIGN) * SLICE_ALIGN
-        # bytes of my column slice of each cell (the last slice may be short)
+        L = _lib.load()
+        self.W = int(L.redset_hip_shard_slice_bytes(chunk, world))
         self.my_len = self.slice_len(rank)
-        self.backend = backend if backend is not None else HipBackend(p, e)
         self._place()
         self.timing = self.device.type == "cuda"
         self._events = []
-        self._gather_ops = None
-        self._return_ops = None
-        d, W, ph = self.d, self.W, p  # every GPU hosts p members
+        d, W, mh = self.d, self.W, p  # every GPU hosts p members
         u8 = dict(dtype=torch.uint8, device=self.device)
-        self.D_host = torch.zeros(world, ph, d, W, **u8)
-        self.P_host = torch.zeros(world, ph, e, W, **u8)
-        self.D_gath = torch.zeros(world, ph, d, W, **u8)
-        self.P_gath = torch.zeros(world, ph, e, W, **u8)
+        self.D_host = torch.zeros(world, mh, d, W, **u8)
+        self.P_host = torch.zeros(world, mh, e, W, **u8)
+        self.D_gath = torch.zeros(world, mh, d, W, **u8)
+        self.P_gath = torch.zeros(world, mh, e, W, **u8)
         if fill:
             g = torch.Generator(device=self.device)
             g.manual_seed(seed + rank)
             self.D_host.copy_(torch.randint(0, 256, self.D_host.shape, generator=g, **u8))
-        # my slice of every stripe of every set, as per-set views
-        self._encode, self._rebuild = [], []
-        for k in range(world):
-            views = self.set_views(k)
-            if self.my_len > 0:
-                self._encode.append(self.backend.prepare_encode(views, self.my_len, W))
-                if self.lost:
-                    self._rebuild.append(self.backend.prepare_rebuild(views, self.lost, self.my_len, W))
+        self._bufs = _Buffers([self.D_host, self.P_host, self.D_gath, self.P_gath])
+        if transport is None:
+            transport = "rccl" if self.device.type == "cuda" and (world == 1 or dist.get_backend() == "nccl") \
+                else "torch"
+        self._transport = RcclTransport(world, rank) if transport == "rccl" else \
+            TorchTransport(world, rank, self._bufs)
+        self._compute = CallbackCompute(backend, p, self._bufs) if backend is not None else None
+        self._codec_h = c_void_p()
+        _lib.check(L.redset_hip_rs_create(p, e, ctypes.byref(self._codec_h)), "rs_create")
+        nm = world * p
+        self._host_arr = (c_int * nm)(*[self._where[m][0] for m in range(nm)])
+        self._slot_arr = (c_int * nm)(*[self._where[m][1] for m in range(nm)])
+        self._layout = _lib.ShardLayout(world, self._host_arr, self._slot_arr, mh, chunk, W,
+                                        self.D_host.data_ptr(), self.P_host.data_ptr(),
+                                        self.D_gath.data_ptr(), self.P_gath.data_ptr())
+        self._plans = {"encode": self._plan(_lib.PLAN_RS_ENCODE, [])}
+        if self.lost:
+            self._plans["rebuild"] = self._plan(_lib.PLAN_RS_REBUILD, self.lost)
+
+    def _plan(self, kind: int, lost: List[int]) -> c_void_p:
+        L = _lib.load()
+        arr = (c_int * max(1, len(lost)))(*lost)
+        h = c_void_p()
+        comp = ctypes.byref(self._compute.struct) if self._compute is not None else None
+        _lib.check(L.redset_hip_rs_sharded_plan(self._codec_h, kind, len(lost), arr, ctypes.byref(self._layout),
+                                                ctypes.byref(self._transport.struct), comp, ctypes.byref(h)),
+                   "rs_sharded_plan")
+        return h
+
+    def info(self, op: str) -> dict:
+        inf = _lib.ShardedInfo()
+        _lib.check(_lib.load().redset_hip_sharded_get_info(self._plans[op], ctypes.byref(inf)), "sharded_get_info")
+        return inf.as_dict()
+
+    def close(self):
+        L = _lib.load()
+        for h in self._plans.values():
+            L.redset_hip_sharded_destroy(h)
+        self._plans = {}
+        self._transport.close()
+        if self._codec_h:
+            L.redset_hip_rs_destroy(self._codec_h)
+            self._codec_h = None
 
     # ---- placement -------------------------------------------------------
     def _place(self) -> None:
@@ -167,119 +258,29 @@ class ShardedSetRunner:
         """(GPU, hosted index) of member r of set k."""
         return self._where[k * self.p + r]
 
-    def set_views(self, k: int) -> SetViews:
-        lofi, parity = [], []
-        for r in range(self.p):
-            h, j = self.host_of(k, r)
-            lofi.append(self.D_gath[h, j].view(-1))
-            parity.append(self.P_gath[h, j].view(-1))
-        return SetViews(lofi, parity)
-
-    # ---- exchanges -------------------------------------------------------
-    def _all_to_all(self, out: torch.Tensor, inp: torch.Tensor) -> None:
-        """out[h] <- inp[me] of rank h, for every h (encode: every cell)."""
-        if self.world == 1:
-            out.copy_(inp)
-            return
-        dist.all_to_all_single(out, inp)
-
-    def _build_rebuild_gather(self) -> None:
-        """The rebuild's gather as one batch of P2P ops: my column slice of
-        every cell some decode reads (rebuild_inputs), from every survivor's
-        host. Lost members are hosted last and never sent; parity rows no
-        decode selects stay home. Cells are flattened per GPU as
-        (hosted member, cell), so neighbouring needed cells merge into one op."""
-        p, d, e, W, me = self.p, self.d, self.e, self.W, self.rank
-        need_d, need_p = rebuild_inputs(p, e, self.lost)
-
-        def runs(h):
-            alive = self._hosted[h][:self.n_alive[h]]
-            fd = [bool(need_d[m % p, s]) for m in alive for s in range(d)]
-            fp = [bool(need_p[m % p, i]) for m in alive for i in range(e)]
-            return _runs(fd), _runs(fp)
-
-        def rows(t, g):  # GPU g's slab of t as [hosted member * cell, W]
-            return t[g].view(-1, W)
-
-        self._gather_local = []
-        self._gather_ops = []
-        self._gather_sent = 0
-        my_d, my_p = runs(me)
-        for a, b in my_d:
-            self._gather_local.append((rows(self.D_gath, me)[a:b], rows(self.D_host, me)[a:b]))
-        for a, b in my_p:
-            self._gather_local.append((rows(self.P_gath, me)[a:b], rows(self.P_host, me)[a:b]))
-        for g in range(self.world):
-            if g == me:
-                continue
-            for a, b in my_d:
-                self._gather_ops.append(dist.P2POp(dist.isend, rows(self.D_host, g)[a:b], g))
-                self._gather_sent += (b - a) * W
-            for a, b in my_p:
-                self._gather_ops.append(dist.P2POp(dist.isend, rows(self.P_host, g)[a:b], g))
-                self._gather_sent += (b - a) * W
-            their_d, their_p = runs(g)
-            for a, b in their_d:
-                self._gather_ops.append(dist.P2POp(dist.irecv, rows(self.D_gath, g)[a:b], g))
-            for a, b in their_p:
-                self._gather_ops.append(dist.P2POp(dist.irecv, rows(self.P_gath, g)[a:b], g))
-
-    def _gather_rebuild_inputs(self) -> None:
-        if self._gather_ops is None:
-            self._build_rebuild_gather()
-        for dst, src in self._gather_local:
-            dst.copy_(src)
-        if self._gather_ops:
-            for req in dist.batch_isend_irecv(self._gather_ops):
-                req.wait()
-
+    # ---- operations ------------------------------------------------------
     def _mark(self, name: str) -> None:
         if self.timing:
             ev = torch.cuda.Event(enable_timing=True)
             ev.record()
             self._events.append((name, ev))
 
-    def _build_return(self) -> None:
-        """Rebuilt slices of lost members go to their hosts (the reference's
-        gather to the failed ranks, src/redset_reedsolomon.c:713-733): my own
-        slice is a local copy, the others arrive from their peers."""
-        self._return_local, self._return_ops, self._return_sent = [], [], 0
-        for k in range(self.world):
-            for r in self.lost:
-                h, j = self.host_of(k, r)
-                if h == self.rank:
-                    self._return_local.append((self.D_host[self.rank, j], self.D_gath[h, j]))
-                    self._return_local.append((self.P_host[self.rank, j], self.P_gath[h, j]))
-                    for g in range(self.world):
-                        if g != self.rank:
-                            self._return_ops.append(dist.P2POp(dist.irecv, self.D_host[g, j], g))
-                            self._return_ops.append(dist.P2POp(dist.irecv, self.P_host[g, j], g))
-                else:
-                    self._return_ops.append(dist.P2POp(dist.isend, self.D_gath[h, j], h))
-                    self._return_ops.append(dist.P2POp(dist.isend, self.P_gath[h, j], h))
-                    self._return_sent += self.D_gath[h, j].numel() + self.P_gath[h, j].numel()
+    def _run(self, op: str) -> None:
+        L = _lib.load()
+        h = self._plans[op]
+        stream = torch.cuda.current_stream().cuda_stream if self.device.type == "cuda" else None
+        self._mark(f"{op}_start")
+        _lib.check(L.redset_hip_sharded_execute_phase(h, _lib.PHASE_GATHER, stream), f"sharded {op} gather")
+        self._mark(f"{op}_gathered")
+        _lib.check(L.redset_hip_sharded_execute_phase(h, _lib.PHASE_COMPUTE, stream), f"sharded {op} compute")
+        self._mark(f"{op}_computed")
+        _lib.check(L.redset_hip_sharded_execute_phase(h, _lib.PHASE_RETURN, stream), f"sharded {op} return")
+        self._mark(f"{op}_done")
 
-    def _return_lost(self) -> None:
-        if self._return_ops is None:
-            self._build_return()
-        for dst, src in self._return_local:
-            dst.copy_(src)
-        if self._return_ops:
-            for req in dist.batch_isend_irecv(self._return_ops):
-                req.wait()
-
-    # ---- operations ------------------------------------------------------
     def encode(self) -> None:
         """Parity of every stripe of every set: gather data slices, compute my
         column slice, return parity slices to their hosts."""
-        self._mark("encode_start")
-        self._all_to_all(self.D_gath, self.D_host)
-        self._mark("encode_gathered")
-        for fn in self._encode:
-            fn()
-        self._mark("encode_computed")
-        self._all_to_all(self.P_host, self.P_gath)
-        self._mark("encode_done")
+        self._run("encode")
 
     def erase(self) -> None:
         """Model the loss of the lost members' files on their hosts."""
@@ -292,14 +293,7 @@ class ShardedSetRunner:
 
     def rebuild(self) -> None:
         """Rebuild the lost members of every set from the survivors."""
-        self._mark("rebuild_start")
-        self._gather_rebuild_inputs()
-        self._mark("rebuild_gathered")
-        for fn in self._rebuild:
-            fn()
-        self._mark("rebuild_computed")
-        self._return_lost()
-        self._mark("rebuild_done")
+        self._run("rebuild")
 
     def step(self) -> None:
         self.encode()
@@ -342,16 +336,15 @@ class ShardedSetRunner:
         return {"encode": enc, "rebuild": reb, "step": enc + reb}[op]
 
     def exchanged_bytes(self, op: str = "step") -> int:
-        """Bytes this GPU sends over the fabric per operation."""
-        if self.world == 1:
-            return 0
-        if self._gather_ops is None:
-            self._build_rebuild_gather()
-        if self._return_ops is None:
-            self._build_return()
-        enc = (self.world - 1) * (self.D_host[0].numel() + self.P_host[0].numel())
-        reb = self._gather_sent + self._return_sent
-        return {"encode": enc, "rebuild": reb, "step": enc + reb}[op]
+        """Bytes this GPU sends over the fabric per operation (C planner's count)."""
+        def sent(o):
+            if o not in self._plans:
+                return 0
+            i = self.info(o)
+            return i["gather_bytes_sent"] + i["return_bytes_sent"]
+        if op == "step":
+            return sent("encode") + sent("rebuild")
+        return sent(op)
 
     def phase_ms(self) -> dict:
         """Mean milliseconds per phase over the steps marked so far."""
@@ -370,8 +363,10 @@ class ShardedSetRunner:
         self._events = []
 
     def report(self, step_seconds: float, op: str = "step") -> dict:
-        coll = {"encode": "RCCL all_to_all (data slices, then parity slices)",
-                "rebuild": "batched RCCL P2P: decode inputs' slices in, rebuilt slices back to their hosts"}
+        tname = type(self._transport).__name__
+        coll = {"encode": f"{tname}: grouped P2P, data slices in, parity slices back (redset_hip_rs_sharded_plan)",
+                "rebuild": f"{tname}: grouped P2P, decode inputs' slices in, rebuilt slices back to their hosts "
+                           "(redset_hip_rs_sharded_plan)"}
         phases = self.phase_ms() if self.timing else None
         out = {
             "exchange": {
@@ -382,17 +377,14 @@ class ShardedSetRunner:
             },
             "per_gpu_GBps": round(self.algorithmic_bytes(op) / step_seconds / 1e9, 2),
         }
-        if phases and op == "rebuild" and self.world > 1:
+        if phases and op in self._plans and self.world > 1:
             # rank 0's send rate over the fabric in each exchange phase (what
             # bounds the sharded rebuild; compare with xGMI, 7 links per GPU)
-            if self._gather_ops is None:
-                self._build_rebuild_gather()
-            if self._return_ops is None:
-                self._build_return()
-            g_ms = phases.get("rebuild_start->gathered")
-            r_ms = phases.get("rebuild_computed->done")
-            out["exchange"]["gather_send_GBps_rank0"] = (round(self._gather_sent / (g_ms * 1e-3) / 1e9, 1)
+            i = self.info(op)
+            g_ms = phases.get(f"{op}_start->gathered")
+            r_ms = phases.get(f"{op}_computed->done")
+            out["exchange"]["gather_send_GBps_rank0"] = (round(i["gather_bytes_sent"] / (g_ms * 1e-3) / 1e9, 1)
                                                          if g_ms else None)
-            out["exchange"]["return_send_GBps_rank0"] = (round(self._return_sent / (r_ms * 1e-3) / 1e9, 1)
-                                                         if r_ms and self._return_sent else None)
+            out["exchange"]["return_send_GBps_rank0"] = (round(i["return_bytes_sent"] / (r_ms * 1e-3) / 1e9, 1)
+                                                         if r_ms and i["return_bytes_sent"] else None)
         return out

@@ -1,0 +1,218 @@
+/*
+ * sharded_test.c -- the sharded encode / rebuild of include/redset_hip.h
+ * under mpirun on CPU: every MPI process is one "GPU" of the node, the C
+ * planner (redset_hip_rs_sharded_plan) moves column slices through the MPI
+ * transport (redset_hip_mpi_transport_*, host buffers) and the compute is a
+ * callback into the CPU oracle (test infrastructure), so the placement, the
+ * slicing and both exchanges are checked against the oracle's whole-set
+ * encode / rebuild without a GPU.
+ *
+ * usage: sharded_test [--gpu] <p> <e> <chunk> [lost ranks...]   (world = MPI size)
+ * --gpu: the slabs live in HBM, the compute is the HIP gf_mac plans and the
+ * MPI transport stages through pinned host memory (every process may share
+ * one GPU) -- the whole sharded path with the real kernels at world > 1.
+ * Placement: `world` sets of p members, member m on process (m * 7 + 3) %
+ * world, hosted slots in ascending member order. Exit 0 iff every process
+ * found its hosted parity (after encode) and its lost members' cells (after
+ * rebuild) equal to the oracle's.
+ */
+#include <hip/hip_runtime_api.h>
+#include <mpi.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include "redset_hip.h"
+#include "redset_hip_mpi.h"
+#include "redset_oracle.h"
+
+static int P, E, D;
+static ro_rs* ORACLE;
+
+static uint8_t byte_of(int k, int r, size_t i) { /* member (k, r)'s logical-file byte i */
+  uint64_t z = ((uint64_t) k << 48) ^ ((uint64_t) r << 32) ^ (uint64_t) i ^ 0x5EEDULL;
+  z += 0x9E3779B97F4A7C15ULL;
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
+  return (uint8_t) (z ^ (z >> 31));
+}
+
+/* compute callback: the oracle on compacted copies of the slices */
+static int oracle_run(void* ctx, int kind, int missing, const int* lost, unsigned char* const* lofi,
+                      unsigned char* const* parity, size_t n, size_t W, void* stream) {
+  uint8_t** lf = malloc(sizeof(*lf) * P);
+  uint8_t** pr = malloc(sizeof(*pr) * P);
+  for (int r = 0; r < P; ++r) {
+    lf[r] = malloc((size_t) D * n + 1);
+    pr[r] = malloc((size_t) E * n + 1);
+    for (int s = 0; s < D; ++s) memcpy(lf[r] + (size_t) s * n, lofi[r] + (size_t) s * W, n);
+    for (int i = 0; i < E; ++i) memcpy(pr[r] + (size_t) i * n, parity[r] + (size_t) i * W, n);
+  }
+  int rc = 0;
+  if (kind == REDSET_HIP_PLAN_RS_ENCODE) ro_rs_encode_set(ORACLE, n, lf, pr, 1 << 20);
+  else rc = ro_rs_rebuild_set(ORACLE, n, missing, lost, lf, pr, 1 << 20);
+  for (int r = 0; r < P; ++r) {
+    for (int s = 0; s < D; ++s) memcpy(lofi[r] + (size_t) s * W, lf[r] + (size_t) s * n, n);
+    for (int i = 0; i < E; ++i) memcpy(parity[r] + (size_t) i * W, pr[r] + (size_t) i * n, n);
+    free(lf[r]);
+    free(pr[r]);
+  }
+  free(lf);
+  free(pr);
+  return rc;
+}
+
+int main(int argc, char** argv) {
+  MPI_Init(&argc, &argv);
+  int world, me;
+  MPI_Comm_size(MPI_COMM_WORLD, &world);
+  MPI_Comm_rank(MPI_COMM_WORLD, &me);
+  const int gpu = argc > 1 && strcmp(argv[1], "--gpu") == 0;
+  if (gpu) {
+    --argc;
+    ++argv;
+  }
+  if (argc < 4) MPI_Abort(MPI_COMM_WORLD, 2);
+  P = atoi(argv[1]);
+  E = atoi(argv[2]);
+  D = P - E;
+  const size_t C = (size_t) atoll(argv[3]);
+  const int missing = argc - 4;
+  int lost[64];
+  for (int i = 0; i < missing; ++i) lost[i] = atoi(argv[4 + i]);
+  ORACLE = ro_rs_new(P, E);
+
+  const int nsets = world, nm = nsets * P;
+  int* host = malloc(sizeof(int) * nm);
+  int* slot = malloc(sizeof(int) * nm);
+  int* count = calloc(world, sizeof(int));
+  int mh = 0;
+  for (int m = 0; m < nm; ++m) {
+    host[m] = (m * 7 + 3) % world;
+    slot[m] = count[host[m]]++;
+    if (count[host[m]] > mh) mh = count[host[m]];
+  }
+  const size_t W = redset_hip_shard_slice_bytes(C, world);
+  const size_t hd = (size_t) world * mh * D * W, hp = (size_t) world * mh * E * W;
+  uint8_t* HD = calloc(hd, 1);
+  uint8_t* HP = calloc(hp, 1);
+  uint8_t* GD = calloc(hd, 1);
+  uint8_t* GP = calloc(hp, 1);
+  /* my hosted members' slabs: slice q of data cell s */
+  for (int m = 0; m < nm; ++m) {
+    if (host[m] != me) continue;
+    for (int q = 0; q < world; ++q)
+      for (int s = 0; s < D; ++s)
+        for (size_t b = 0; b < W && q * W + b < C; ++b)
+          HD[(((size_t) q * mh + slot[m]) * D + s) * W + b] = byte_of(m / P, m % P, s * C + q * W + b);
+  }
+  /* the oracle's whole-set answer for every set */
+  uint8_t** want_l = malloc(sizeof(uint8_t*) * nm);
+  uint8_t** want_p = malloc(sizeof(uint8_t*) * nm);
+  for (int m = 0; m < nm; ++m) {
+    want_l[m] = malloc((size_t) D * C);
+    want_p[m] = calloc((size_t) E * C, 1);
+    for (size_t i = 0; i < (size_t) D * C; ++i) want_l[m][i] = byte_of(m / P, m % P, i);
+  }
+  for (int k = 0; k < nsets; ++k) ro_rs_encode_set(ORACLE, C, want_l + k * P, want_p + k * P, 1 << 20);
+
+  redset_hip_rs* rs = NULL;
+  redset_hip_transport tr;
+  redset_hip_mpi_transport* th = NULL;
+  redset_hip_compute comp = {oracle_run, NULL};
+  redset_hip_shard_layout L = {nsets, host, slot, mh, C, W, HD, HP, GD, GP};
+  uint8_t *dHD = NULL, *dHP = NULL, *dGD = NULL, *dGP = NULL;
+  hipStream_t stream = NULL;
+  if (gpu) {
+    if (hipMalloc((void**) &dHD, hd) || hipMalloc((void**) &dHP, hp) || hipMalloc((void**) &dGD, hd) ||
+        hipMalloc((void**) &dGP, hp) || hipStreamCreate(&stream) || hipMemcpy(dHD, HD, hd, hipMemcpyHostToDevice) ||
+        hipMemset(dHP, 0, hp) || hipMemset(dGD, 0, hd) || hipMemset(dGP, 0, hp)) {
+      fprintf(stderr, "rank %d: device setup failed\n", me);
+      MPI_Abort(MPI_COMM_WORLD, 3);
+    }
+    L.hosted_data = dHD;
+    L.hosted_parity = dHP;
+    L.gathered_data = dGD;
+    L.gathered_parity = dGP;
+  }
+  redset_hip_sharded *enc = NULL, *reb = NULL;
+  const redset_hip_compute* cp = gpu ? NULL : &comp;
+  int ok = redset_hip_rs_create(P, E, &rs) == 0 && redset_hip_mpi_transport_create(MPI_COMM_WORLD, gpu, &tr, &th) == 0 &&
+           redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, &tr, cp, &enc) == 0 &&
+           (missing == 0 ||
+            redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, &tr, cp, &reb) == 0);
+  if (!ok) fprintf(stderr, "rank %d: setup: %s\n", me, redset_hip_last_error());
+  int bad = 0;
+  if (ok && redset_hip_sharded_execute(enc, stream) != 0) {
+    fprintf(stderr, "rank %d: encode: %s\n", me, redset_hip_last_error());
+    ok = 0;
+  }
+  if (gpu && (hipStreamSynchronize(stream) || hipMemcpy(HP, dHP, hp, hipMemcpyDeviceToHost))) ok = 0;
+  /* compare my hosted members' parity slabs with the oracle */
+  for (int m = 0; ok && m < nm; ++m) {
+    if (host[m] != me) continue;
+    for (int q = 0; q < world; ++q)
+      for (int i = 0; i < E; ++i)
+        for (size_t b = 0; b < W && q * W + b < C; ++b)
+          bad += HP[(((size_t) q * mh + slot[m]) * E + i) * W + b] != want_p[m][i * C + q * W + b];
+  }
+  if (bad) fprintf(stderr, "rank %d: %d parity bytes differ from the oracle\n", me, bad);
+  if (ok && reb) {
+    /* lose the members, scribble on the gathered slots, rebuild */
+    for (int m = 0; m < nm; ++m) {
+      int is_lost = 0;
+      for (int i = 0; i < missing; ++i) is_lost |= lost[i] == m % P;
+      if (!is_lost || host[m] != me) continue;
+      for (int q = 0; q < world; ++q) {
+        memset(HD + (((size_t) q * mh + slot[m]) * D) * W, 0xEE, (size_t) D * W);
+        memset(HP + (((size_t) q * mh + slot[m]) * E) * W, 0xEE, (size_t) E * W);
+      }
+    }
+    memset(GD, 0xA5, hd);
+    memset(GP, 0x5A, hp);
+    if (gpu && (hipMemcpy(dHD, HD, hd, hipMemcpyHostToDevice) || hipMemcpy(dHP, HP, hp, hipMemcpyHostToDevice) ||
+                hipMemset(dGD, 0xA5, hd) || hipMemset(dGP, 0x5A, hp)))
+      ok = 0;
+    if (ok && redset_hip_sharded_execute(reb, stream) != 0) {
+      fprintf(stderr, "rank %d: rebuild: %s\n", me, redset_hip_last_error());
+      ok = 0;
+    }
+    if (gpu && (hipStreamSynchronize(stream) || hipMemcpy(HD, dHD, hd, hipMemcpyDeviceToHost) ||
+                hipMemcpy(HP, dHP, hp, hipMemcpyDeviceToHost)))
+      ok = 0;
+    int rbad = 0;
+    for (int m = 0; ok && m < nm; ++m) {
+      if (host[m] != me) continue;
+      for (int q = 0; q < world; ++q)
+        for (size_t b = 0; b < W && q * W + b < C; ++b) {
+          for (int s = 0; s < D; ++s)
+            rbad += HD[(((size_t) q * mh + slot[m]) * D + s) * W + b] != want_l[m][s * C + q * W + b];
+          for (int i = 0; i < E; ++i)
+            rbad += HP[(((size_t) q * mh + slot[m]) * E + i) * W + b] != want_p[m][i * C + q * W + b];
+        }
+    }
+    if (rbad) fprintf(stderr, "rank %d: %d bytes differ after the rebuild\n", me, rbad);
+    bad += rbad;
+    redset_hip_sharded_info info;
+    if (ok && redset_hip_sharded_get_info(reb, &info) == 0)
+      printf("rank %d: rebuild gather %llu B sent in %d messages, return %llu B sent, local %llu B\n", me,
+             info.gather_bytes_sent, info.gather_messages, info.return_bytes_sent, info.local_bytes);
+  }
+  int mine = ok && !bad, all = 0;
+  MPI_Allreduce(&mine, &all, 1, MPI_INT, MPI_LAND, MPI_COMM_WORLD);
+  redset_hip_sharded_destroy(enc);
+  redset_hip_sharded_destroy(reb);
+  redset_hip_mpi_transport_destroy(th);
+  redset_hip_rs_destroy(rs);
+  if (gpu) {
+    (void) hipFree(dHD);
+    (void) hipFree(dHP);
+    (void) hipFree(dGD);
+    (void) hipFree(dGP);
+    (void) hipStreamDestroy(stream);
+  }
+  ro_rs_delete(ORACLE);
+  MPI_Finalize();
+  return all ? 0 : 1;
+}

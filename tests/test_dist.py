@@ -1,8 +1,9 @@
-"""World-size-2 (and 3) gloo tests of the multi-GPU exchange logic in
-redset_amd.dist on CPU. The HIP compute is replaced by a CPU checker backend
-(the oracle) so that these tests exercise only the placement, the column
-slicing and the all-to-all / P2P exchanges; tests/test_gpu_parity.py covers
-the HIP compute."""
+"""World-size 2/3/4/8 gloo tests of the sharded path on CPU: the C ABI's
+planner (redset_hip_rs_sharded_plan, redset_amd/csrc/sharded.c) drives a
+torch.distributed (gloo) callback transport, and the HIP compute is replaced
+by a CPU checker callback (the oracle), so these tests exercise the C
+placement, column slicing and exchange plans; tests/test_gpu_parity.py covers
+the HIP compute with the RCCL transport."""
 import os
 import socket
 import tempfile
@@ -17,7 +18,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 class OracleBackend:
-    """CPU stand-in for HipBackend, built on the oracle (test-only)."""
+    """CPU stand-in for the HIP compute of the sharded plan (the C ABI's
+    redset_hip_compute callback), built on the oracle (test-only)."""
 
     def __init__(self, p, e):
         import oracle_lib
@@ -25,30 +27,22 @@ class OracleBackend:
         self.st = oracle_lib.OracleRS(p, e)
         self.p, self.e = p, e
 
-    def _compact(self, views, n, W):
-        lofi = [np.ascontiguousarray(t.numpy().reshape(-1, W)[:, :n]).reshape(-1) for t in views.lofi]
-        parity = [np.ascontiguousarray(t.numpy().reshape(-1, W)[:, :n]).reshape(-1) for t in views.parity]
-        return lofi, parity
+    def run(self, kind, lost, lofi, parity, n, W, bufs):
+        from redset_amd import _lib
 
-    def _scatter(self, views, lofi, parity, n, W):
-        for t, a in zip(views.lofi, lofi):
-            t.numpy().reshape(-1, W)[:, :n] = a.reshape(-1, n)
-        for t, a in zip(views.parity, parity):
-            t.numpy().reshape(-1, W)[:, :n] = a.reshape(-1, n)
-
-    def prepare_encode(self, views, n, W):
-        def run():
-            lofi, parity = self._compact(views, n, W)
-            self.st.encode_set(lofi, parity, n)
-            self._scatter(views, lofi, parity, n, W)
-        return run
-
-    def prepare_rebuild(self, views, lost, n, W):
-        def run():
-            lofi, parity = self._compact(views, n, W)
-            assert self.st.rebuild_set(list(lost), lofi, parity, n) == 0
-            self._scatter(views, lofi, parity, n, W)
-        return run
+        d, e = self.p - self.e, self.e
+        lv = [bufs.view(a, d * W).numpy().reshape(d, W) for a in lofi]
+        pv = [bufs.view(a, e * W).numpy().reshape(e, W) for a in parity]
+        lf = [np.ascontiguousarray(v[:, :n]).reshape(-1) for v in lv]
+        pr = [np.ascontiguousarray(v[:, :n]).reshape(-1) for v in pv]
+        if kind == _lib.PLAN_RS_ENCODE:
+            self.st.encode_set(lf, pr, n)
+        else:
+            assert self.st.rebuild_set(list(lost), lf, pr, n) == 0
+        for v, a in zip(lv, lf):
+            v[:, :n] = a.reshape(d, n)
+        for v, a in zip(pv, pr):
+            v[:, :n] = a.reshape(e, n)
 
 
 def _free_port():
@@ -68,7 +62,7 @@ def _worker(rank, world, port, p, e, chunk, lost, outdir):
     from redset_amd.dist import ShardedSetRunner
 
     runner = ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, device="cpu",
-                              backend=OracleBackend(p, e), seed=99)
+                              backend=OracleBackend(p, e), seed=99, transport="torch")
     if rank == 0:
         import json
 

@@ -151,3 +151,21 @@ def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=90, env={**os.environ, **env})
     assert res.returncode != 0, res.stdout + res.stderr  # every rank exits 1 (alltrue is false)
     assert "backend failed" in res.stderr
+
+
+@pytest.mark.parametrize("np_,p,e,chunk,lost", [(2, 11, 3, 300_001, [1, 2]), (4, 20, 4, 65536, [0, 5, 19]),
+                                                 (3, 6, 3, 1000, [2])])
+def test_mpi_sharded_gpu(np_, p, e, chunk, lost):
+    """The sharded path with the real HIP kernels at world > 1: slabs in HBM,
+    gf_mac plans over each process's column slice, the MPI transport staging
+    through pinned memory (the processes share the box's one GPU; RCCL needs
+    one GPU per rank). tests/mpi/sharded_test.c --gpu checks hosted parity and
+    the rebuilt members against the oracle."""
+    driver = os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
+    if not _have() or not os.path.exists(driver):
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/sharded_test")
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", driver, "--gpu", str(p), str(e), str(chunk)] + \
+        [str(x) for x in lost]
+    res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert res.stdout.count("rebuild gather") == np_

@@ -427,8 +427,10 @@ def test_full_size_xor_c2(rd, oracle):
 
 
 def test_sharded_runner_world1_hip(rd, oracle):
-    """redset_amd.dist with the HIP backend at world size 1 (no exchange):
-    column-slab layout + plans over gathered slices, checked against the oracle."""
+    """redset_amd.dist at world size 1: the C sharded plan (column-slab
+    layout, HIP plans over gathered slices) with the RCCL transport (a
+    one-rank communicator; the exchanges are local copies), checked against
+    the oracle."""
     from redset_amd.dist import ShardedSetRunner
 
     p, e, chunk = 11, 3, 300_000

@@ -117,7 +117,7 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf):
     ("rs", "rebuild", {"RANK_TEST_FAIL_READ": "3"}),
     ("rs", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "0"}),
     ("xor", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2"}),
-    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "1"}),
+    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2"}),  # the root runs the GPU work
     ("xor", "rebuild", {"RANK_TEST_FAIL_READ": "0"}),
 ])
 def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme, op, env):

@@ -231,3 +231,64 @@ def test_short_survivor_file_fails_the_rebuild(rd, oracle, tmp_path, victim):
     with pytest.raises(redset_amd.RedsetHipError, match="I/O"):
         stream.rs_rebuild_stream(codec, lost, chunk, io, slice_bytes=16384)
     io.close()
+
+
+@pytest.mark.slow
+def test_config4_full_chunk_stream_windows_and_round_trip(rd, oracle):
+    """BASELINE.json configs[4] at its own sizes: RS(16+4), p = 20, 256 MiB
+    chunks, host-resident cells streamed through the pinned pipeline
+    (redset_hip_rs_encode_stream / _rebuild_stream). Three of the 20 stripes
+    run (the pipeline takes a stripe range; every stripe reads a cell of every
+    member, so the whole set's layout is addressed): their parity is checked
+    against the oracle on random byte windows, then four members' cells of
+    those stripes are erased and rebuilt bit for bit. Cells of other stripes
+    are never touched (their host pages are never committed)."""
+    redset_amd, stream = rd
+    p, e, C = 20, 4, 256 << 20
+    d = p - e
+    stripes = [0, 7, 19]
+    lofi = [np.empty(d * C, np.uint8) for _ in range(p)]
+    parity = [np.empty(e * C, np.uint8) for _ in range(p)]
+    codec = redset_amd.RSCodec(p, e)
+    rng = np.random.default_rng(2024)
+    cells = {}  # (member, kind, index) -> view of every cell the chosen stripes touch
+    for c in stripes:
+        for r in range(p):
+            enc = codec.encoding_id(r, c)
+            if enc < p:
+                k = codec.data_id(r, c)
+                v = lofi[r][k * C:(k + 1) * C]
+                v[:] = np.frombuffer(rng.bytes(C), np.uint8)
+                cells[(r, 0, k)] = v
+            else:
+                v = parity[r][(enc - p) * C:(enc - p + 1) * C]
+                v[:] = 0
+                cells[(r, 1, enc - p)] = v
+    io = stream.HostIO(p, [a.ctypes.data for a in lofi], [a.ctypes.data for a in parity], C,
+                       keepalive=(lofi, parity))
+    for c in stripes:
+        st = stream.rs_encode_stream(codec, C, io, first=c, nstripes=1)
+        assert st["bytes_written"] == e * C
+    # oracle on byte windows of the chosen stripes (parity is byte-wise)
+    orc = oracle.OracleRS(p, e)
+    for _ in range(6):
+        w = int(rng.integers(1, 4096))
+        off = int(rng.integers(0, C - w))
+        lw = [np.zeros(d * w, np.uint8) for _ in range(p)]
+        pw = [np.zeros(e * w, np.uint8) for _ in range(p)]
+        for (r, kind, k), v in cells.items():
+            if kind == 0:
+                lw[r][k * w:(k + 1) * w] = v[off:off + w]
+        orc.encode_set(lw, pw, w)
+        for (r, kind, k), v in cells.items():
+            if kind == 1:
+                assert np.array_equal(v[off:off + w], pw[r][k * w:(k + 1) * w]), (r, k, off, w)
+    # lose four members, rebuild the chosen stripes
+    lost = [0, 5, 13, 19]
+    snap = {key: v.copy() for key, v in cells.items() if key[0] in lost}
+    for key in snap:
+        cells[key][:] = 0xEE
+    for c in stripes:
+        stream.rs_rebuild_stream(codec, lost, C, io, first=c, nstripes=1)
+    for key, want in snap.items():
+        assert np.array_equal(cells[key], want), key

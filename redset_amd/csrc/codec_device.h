@@ -76,6 +76,15 @@
 #ifndef REDSET_WAVES_PER_EU
 #define REDSET_WAVES_PER_EU 2
 #endif
+// LDS-DMA input ring (A/B knob, 0 = off): every wave streams its inputs
+// with global_load_lds_dwordx4 into a private ring of REDSET_GLDS stages in
+// LDS (no VGPR destination, no barrier), waits for the oldest stage with a
+// counted vmcnt and reads it back with ds_read_b128; stores as the plain
+// sweep. Stages shrink to fit kGldsLdsBudget for wide NIN.
+#ifndef REDSET_GLDS
+#define REDSET_GLDS 0
+#endif
+
 #if REDSET_WAVES_PER_EU > 0
 #define REDSET_KERNEL __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, REDSET_WAVES_PER_EU)))
 #else
@@ -383,6 +392,108 @@ __device__ __forceinline__ void sweep(g_cu4* const (&in)[NIN], size_t nvec, size
   }
 }
 
+#if REDSET_GLDS
+constexpr int kWavesPerBlock = kBlock / 64;
+constexpr int kGldsLdsBudget = 144 * 1024;
+// stages of the ring for NIN inputs: REDSET_GLDS, fewer if the ring would
+// not fit (1 = no overlap inside the wave)
+template <int NIN>
+constexpr int glds_stages() {
+  int st = REDSET_GLDS;
+  while (st > 1 && st * NIN * 1024 * kWavesPerBlock > kGldsLdsBudget) --st;
+  return st;
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// wait until the stage issued `a` load groups and `b` store groups ago has
+// landed: vmcnt counts loads, LDS-DMA and stores together, in issue order
+template <int NIN, int NOUT, int A, int B>
+__device__ __forceinline__ void wait_stage_ab() {
+  wait_vm<A * NIN + B * NOUT>();
+}
+template <int NIN, int NOUT, int S>
+__device__ __forceinline__ void wait_stage(int a, int b) {
+  static_assert(S >= 1 && S <= 3, "ring depth");
+  if constexpr (S == 1) {
+    wait_vm<0>();
+  } else if constexpr (S == 2) {
+    if (a == 1) {
+      if (b == 1) wait_stage_ab<NIN, NOUT, 1, 1>(); else wait_stage_ab<NIN, NOUT, 1, 0>();
+    } else {
+      if (b == 1) wait_stage_ab<NIN, NOUT, 0, 1>(); else wait_stage_ab<NIN, NOUT, 0, 0>();
+    }
+  } else {
+    switch (a * 3 + b) {
+      case 0: wait_stage_ab<NIN, NOUT, 0, 0>(); break;
+      case 1: wait_stage_ab<NIN, NOUT, 0, 1>(); break;
+      case 2: wait_stage_ab<NIN, NOUT, 0, 2>(); break;
+      case 3: wait_stage_ab<NIN, NOUT, 1, 0>(); break;
+      case 4: wait_stage_ab<NIN, NOUT, 1, 1>(); break;
+      case 5: wait_stage_ab<NIN, NOUT, 1, 2>(); break;
+      case 6: wait_stage_ab<NIN, NOUT, 2, 0>(); break;
+      case 7: wait_stage_ab<NIN, NOUT, 2, 1>(); break;
+      default: wait_stage_ab<NIN, NOUT, 2, 2>(); break;
+    }
+  }
+}
+
+typedef __attribute__((address_space(3))) v4u l_u4;
+
+// The wave's positions: base + k * vstep + lane, k < iters. Stage k's NIN
+// loads go to ring slot k % S; position clamped to the last vector (its
+// store skipped) for lanes past the end.
+template <int NIN, int NOUT, bool ACC>
+__device__ __forceinline__ void gf_mac_glds_sweep(const uint32_t* tables, l_u4* ring, g_cu4* const (&in)[NIN],
+                                                  g_u4* const (&out)[NOUT], size_t nvec, size_t vstep, size_t base) {
+  constexpr int S = glds_stages<NIN>();
+  const int lane = threadIdx.x & 63;
+  if (base >= nvec) return;
+  const size_t last = nvec - 1;
+  const int iters = static_cast<int>((nvec - base + vstep - 1) / vstep);
+  // inline asm, not __builtin_amdgcn_global_load_lds: hipcc treats the
+  // builtin as an LDS write on vmcnt and drains vmcnt(0) before the next
+  // ds_read of ANY ring slot, which would serialise the stages; asm LDS-DMA
+  // is invisible to its wait bookkeeping, so wait_stage counts it instead
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>(ring)));
+  auto issue = [&](int k) {
+    const size_t v = base + static_cast<size_t>(k) * vstep + lane;
+    const size_t vc = v < nvec ? v : last;
+    const uint32_t slot = ring0 + static_cast<uint32_t>((k % S) * NIN * 1024);
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) {
+      uint32_t keep;
+      asm volatile(
+          "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+#if REDSET_LOAD_POLICY == 1
+          " nt"
+#endif
+          "\n\ts_mov_b32 m0, %0"
+          : "=&s"(keep)
+          : "v"(in[i] + vc), "s"(slot + static_cast<uint32_t>(i * 1024))
+          : "memory");
+    }
+  };
+  for (int k = 0; k < S - 1 && k < iters; ++k) issue(k);
+  for (int k = 0; k < iters; ++k) {
+    if (k + S - 1 < iters) issue(k + S - 1);
+    // load groups issued after stage k, store groups issued after it
+    const int a = (S - 1) < (iters - 1 - k) ? (S - 1) : (iters - 1 - k);
+    const int b = k < (S - 1) ? k : (S - 1);
+    wait_stage<NIN, NOUT, S>(a, b);
+    const l_u4* slot = ring + (k % S) * NIN * 64;
+    v4u x[NIN];
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) x[i] = slot[i * 64 + lane];
+    const size_t v = base + static_cast<size_t>(k) * vstep + lane;
+    gf_mac_vec<NIN, NOUT, ACC>(tables, x, out, v < nvec ? v : last, v < nvec);
+  }
+}
+#endif
+
 template <int NIN, int NOUT, bool ACC>
 __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, int part) {
   // static (not extern) so the table offsets fold into ds_read's immediate
@@ -400,6 +511,13 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
     g_u4* out[NOUT];
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) out[j] = (g_u4*) (J.out[j]);
+#if REDSET_GLDS
+    __shared__ v4u ring_mem[glds_stages<NIN>() * NIN * 64 * kWavesPerBlock];
+    const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+    l_u4* ring = (l_u4*) (ring_mem) + wave * glds_stages<NIN>() * NIN * 64;
+    gf_mac_glds_sweep<NIN, NOUT, ACC>(lds, ring, in, out, nvec, vstep,
+                                      static_cast<size_t>(part) * kBlock + static_cast<size_t>(wave) * 64);
+#else
     sweep<NIN>(
         in, nvec, vstep, part,
         [&](const v4u (&x)[NIN], size_t v, bool st) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, st); },
@@ -409,6 +527,7 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
             for (int j = 0; j < NOUT; ++j) out[j][v] = v4u{0, 0, 0, 0};
           }
         });
+#endif
   }
 
   // byte path: the tail after the last whole 16-B vector, or everything when

@@ -99,6 +99,8 @@ int main(int argc, char** argv) {
     if (fd < 0 || lseek(fd, (off_t) header, SEEK_SET) < 0) MPI_Abort(MPI_COMM_WORLD, 5);
   }
 
+  MPI_Barrier(MPI_COMM_WORLD);
+  const double t0 = MPI_Wtime();
   if (rs_scheme) {
     redset_hip_rs* rs = NULL;
     rc = redset_hip_rs_create(ranks, encoding, &rs);
@@ -116,6 +118,10 @@ int main(int argc, char** argv) {
   fsync(fd);
   close(fd);
   redset_hip_fileio_destroy(files);
+  /* backend call + fsync of what it wrote, slowest rank (the collective's time) */
+  double dt = MPI_Wtime() - t0, dmax = 0;
+  MPI_Reduce(&dt, &dmax, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+  if (rank == 0) printf("rank_test: %s %s %d ranks chunk %llu buf %zu: %.4f s\n", argv[1], argv[2], ranks, chunk, buf, dmax);
 
   int ok = rc == REDSET_SUCCESS, all = 0;
   MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_LAND, MPI_COMM_WORLD); /* redset_alltrue */

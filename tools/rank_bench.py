@@ -1,0 +1,64 @@
+#!/usr/bin/env python3
+"""Per-rank MPI backends at scale (the drop-in REDSET_ENCODE=HIP path): p
+ranks under mpirun sharing the box's GPU, each with one data file of
+d * chunk bytes, RS encode then rebuild of two lost ranks (rank_test.c =
+redset_apply / redset_recover's calling convention). Prints the slowest
+rank's time per call and the algorithmic rate ((d+e)*C per stripe encode,
+(d+m)*C rebuild, p stripes)."""
+import argparse
+import json
+import os
+import re
+import shutil
+import subprocess
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MIB = 1 << 20
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ranks", type=int, default=11)
+    ap.add_argument("--encoding", type=int, default=3)
+    ap.add_argument("--chunk-mib", type=int, default=16)
+    ap.add_argument("--buf-mib", type=float, default=1.0)
+    ap.add_argument("--lost", default="1,2")
+    ap.add_argument("--dir", default="/tmp/rank_bench")
+    a = ap.parse_args()
+    p, e = a.ranks, a.encoding
+    d, C = p - e, a.chunk_mib * MIB
+    lost = [int(x) for x in a.lost.split(",")]
+    shutil.rmtree(a.dir, ignore_errors=True)
+    os.makedirs(a.dir)
+    block = np.frombuffer(np.random.default_rng(1).bytes(16 * MIB), np.uint8)
+    for r in range(p):
+        path = os.path.join(a.dir, f"r{r}.dat")
+        with open(path, "wb") as f:
+            for k in range(d * C // block.size):
+                f.write(np.roll(block, r * 131 + k).tobytes())
+        with open(os.path.join(a.dir, f"manifest_{r}.txt"), "w") as f:
+            f.write(f"1\n{path} {d * C}\n{C}\n4096\n{os.path.join(a.dir, f'r{r}.rs.redset')}\n")
+    drv = os.path.join(ROOT, "tests", "mpi", "build", "rank_test")
+    buf = int(a.buf_mib * MIB)
+    out = {}
+    for op, extra in (("encode", []), ("rebuild", lost)):
+        if op == "rebuild":
+            for r in lost:
+                os.unlink(os.path.join(a.dir, f"r{r}.dat"))
+                os.unlink(os.path.join(a.dir, f"r{r}.rs.redset"))
+        cmd = ["/opt/conda/bin/mpirun", "-np", str(p), "-host", "localhost", drv, "rs", op, str(e), a.dir, str(buf)] + \
+            [str(x) for x in extra]
+        res = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        if res.returncode != 0:
+            raise SystemExit(res.stdout + res.stderr)
+        t = float(re.search(r": ([0-9.]+) s", res.stdout).group(1))
+        alg = p * (d + (e if op == "encode" else len(lost))) * C
+        out[op] = {"seconds": t, "GBps": round(alg / t / 1e9, 3)}
+    shutil.rmtree(a.dir, ignore_errors=True)
+    print(json.dumps({"ranks": p, "encoding": e, "chunk": C, "buf": buf, **out}))
+
+
+if __name__ == "__main__":
+    main()

@@ -24,8 +24,8 @@
 #include <unistd.h>
 
 #define DEFAULT_BUF ((size_t) 1 << 20) /* redset_mpi_buf_size default, src/redset.c:45 */
-#define MAX_SCRATCH 8
-#define MAX_STAGE ((size_t) 64 << 20) /* RS encode: bytes of ring slices staged per window */
+#define MAX_SCRATCH 12
+#define MAX_STAGE ((size_t) 32 << 20) /* RS encode: bytes of ring slices staged per window (x2 buffers) */
 
 static int fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 static int fail(const char* fmt, ...) {
@@ -171,6 +171,13 @@ static int xor_segment(int t, int c) { return c < t ? c : c - 1; }
 
 /* ---- RS encode (replaces redset_reedsolomon_encode, src/redset_reedsolomon.c:280-402) */
 
+/* record / wait an event of the scratch stream; a failure marks the device as gone */
+static int ev_record(scratch* S, hipEvent_t ev) {
+  return hipEventRecord(ev, S->stream) == hipSuccess ? 0 : fail("hipEventRecord failed");
+}
+static int ev_wait(hipEvent_t ev) {
+  return hipEventSynchronize(ev) == hipSuccess ? 0 : fail("device work failed (hipEventSynchronize)");
+}
 
 int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi,
                               const char* chunk_file, int fd_chunk, size_t chunk_size, size_t buf_size) {
@@ -186,7 +193,8 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
   /* ring steps staged per window: the d*e slices of a slice's whole ring
    * would need d*e*B of pinned and device memory (O(p*e)); windows of G steps
-   * bound it to MAX_STAGE, the reference's own scratch being e+e+1 slices */
+   * bound each staging buffer to MAX_STAGE, the reference's own scratch being
+   * e+e+1 slices */
   int G = (int) (MAX_STAGE / ((size_t) e * B));
   if (G < 1) G = 1;
   if (G > d) G = d;
@@ -197,12 +205,20 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
   MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) e);
   scratch S;
   scratch_init(&S);
+  /* two of everything the GPU touches: window w+1's exchange fills one
+   * receive buffer while the GPU copies and combines window w from the other,
+   * and slice n's parity is written while slice n+1 is exchanged */
   uint8_t* h_send = scratch_host(&S, B);
-  uint8_t* h_recv = scratch_host(&S, (size_t) G * e * B); /* [step in window][slot i] */
-  uint8_t* h_par = scratch_host(&S, (size_t) e * B);
-  uint8_t* d_recv = scratch_dev(&S, (size_t) G * e * B);
-  uint8_t* d_par = scratch_dev(&S, (size_t) e * B);
+  uint8_t* h_recv[2] = {scratch_host(&S, (size_t) G * e * B), scratch_host(&S, (size_t) G * e * B)};
+  uint8_t* h_par[2] = {scratch_host(&S, (size_t) e * B), scratch_host(&S, (size_t) e * B)};
+  uint8_t* d_recv[2] = {scratch_dev(&S, (size_t) G * e * B), scratch_dev(&S, (size_t) G * e * B)};
+  uint8_t* d_par[2] = {scratch_dev(&S, (size_t) e * B), scratch_dev(&S, (size_t) e * B)};
+  hipEvent_t ev_recv[2] = {NULL, NULL}, ev_par[2] = {NULL, NULL};
   int rc = S.rc ? S.rc : hrc;
+  for (int k = 0; k < 2 && !rc; ++k)
+    if (hipEventCreateWithFlags(&ev_recv[k], hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&ev_par[k], hipEventDisableTiming) != hipSuccess)
+      rc = fail("hipEventCreate failed");
   if (!rc && (!mat || !coef || !ins || !req)) rc = fail("out of host memory");
   if (!rc) rc = redset_hip_rs_matrix(rs, mat);
   if ((rc = agree_setup(comm, rc))) goto out;
@@ -219,10 +235,21 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
   /* after a device failure the loop keeps every MPI call (peers must not
    * hang, src/redset_reedsolomon.c:338-342) but skips GPU work and writes */
   int dev_failed = 0;
-  for (size_t nread = 0; nread < chunk_size; nread += B) {
+  long wcount = 0;                  /* windows so far (receive buffer = wcount & 1) */
+  int have_prev = 0, prev_sp = 0;   /* a slice whose parity is still to be written */
+  size_t prev_nread = 0, prev_count = 0;
+  size_t n = 0;
+  for (size_t nread = 0; nread < chunk_size; nread += B, ++n) {
     const size_t count = min_sz(B, chunk_size - nread);
+    const int sp = (int) (n & 1);
     for (int s0 = 0; s0 < d; s0 += G) {
       const int gs = d - s0 < G ? d - s0 : G;
+      const int bb = (int) (wcount & 1);
+      /* the copy that read this receive buffer two windows ago is done */
+      if (!dev_failed && wcount >= 2 && ev_wait(ev_recv[bb])) {
+        rc = REDSET_FAILURE;
+        dev_failed = 1;
+      }
       for (int s = s0; s < s0 + gs; ++s) { /* chunk_step = p-1 .. e, src/redset_reedsolomon.c:329-377 */
         const int step = p - 1 - s;
         const int chunk_id = (r + step) % p;
@@ -234,43 +261,72 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
         int k = 0;
         for (int i = 0; i < e; ++i) {
           const int dist = p - step + i;
-          MPI_Irecv(h_recv + ((size_t) (s - s0) * e + i) * B, (int) count, MPI_BYTE, (r + dist) % p, 0, comm,
+          MPI_Irecv(h_recv[bb] + ((size_t) (s - s0) * e + i) * B, (int) count, MPI_BYTE, (r + dist) % p, 0, comm,
                     &req[k++]);
           MPI_Isend(h_send, (int) count, MPI_BYTE, (r - dist + p) % p, 0, comm, &req[k++]);
         }
         MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
       }
+      ++wcount;
       if (dev_failed) continue;
       /* the window's gs*e slices: one H2D, one kernel per slot accumulating
-       * over the window's steps, then wait before h_recv is reused */
+       * over the window's steps -- enqueued, not waited for */
       int grc = injected_device_failure(comm);
-      if (!grc) grc = h2d(&S, d_recv, h_recv, (size_t) gs * e * B);
+      if (!grc) grc = h2d(&S, d_recv[bb], h_recv[bb], (size_t) gs * e * B);
+      if (!grc) grc = ev_record(&S, ev_recv[bb]);
       for (int i = 0; i < e && !grc; ++i) {
-        for (int s = 0; s < gs; ++s) ins[s] = d_recv + ((size_t) s * e + i) * B;
-        unsigned char* o = d_par + (size_t) i * B;
+        for (int s = 0; s < gs; ++s) ins[s] = d_recv[bb] + ((size_t) s * e + i) * B;
+        unsigned char* o = d_par[sp] + (size_t) i * B;
         grc = redset_hip_gf_combine(ins, gs, &o, 1, coef + (size_t) i * d + s0, count, s0 > 0, S.stream);
       }
-      if (!grc) grc = sync_stream(&S);
       if (grc) {
         rc = grc;
         dev_failed = 1;
       }
     }
-    if (dev_failed) continue;
-    int grc = d2h(&S, h_par, d_par, (size_t) e * B);
-    if (!grc) grc = sync_stream(&S);
-    if (grc) {
-      rc = grc;
-      dev_failed = 1;
-      continue;
+    if (!dev_failed) {
+      int grc = d2h(&S, h_par[sp], d_par[sp], (size_t) e * B);
+      if (!grc) grc = ev_record(&S, ev_par[sp]);
+      if (grc) {
+        rc = grc;
+        dev_failed = 1;
+      }
     }
-    for (int i = 0; i < e; ++i) { /* :379-388 */
-      const off_t off = header + (off_t) i * (off_t) chunk_size + (off_t) nread;
-      if (pwrite_full(fd_chunk, h_par + (size_t) i * B, count, off) != 0) rc = fail("write %s failed", chunk_file);
+    /* the previous slice's parity, while this slice's GPU work runs (:379-388) */
+    if (have_prev && !dev_failed) {
+      if (ev_wait(ev_par[prev_sp])) {
+        rc = REDSET_FAILURE;
+        dev_failed = 1;
+      } else {
+        for (int i = 0; i < e; ++i) {
+          const off_t off = header + (off_t) i * (off_t) chunk_size + (off_t) prev_nread;
+          if (pwrite_full(fd_chunk, h_par[prev_sp] + (size_t) i * B, prev_count, off) != 0)
+            rc = fail("write %s failed", chunk_file);
+        }
+      }
+    }
+    have_prev = 1;
+    prev_sp = sp;
+    prev_nread = nread;
+    prev_count = count;
+  }
+  if (have_prev && !dev_failed) {
+    if (ev_wait(ev_par[prev_sp])) {
+      rc = REDSET_FAILURE;
+    } else {
+      for (int i = 0; i < e; ++i) {
+        const off_t off = header + (off_t) i * (off_t) chunk_size + (off_t) prev_nread;
+        if (pwrite_full(fd_chunk, h_par[prev_sp] + (size_t) i * B, prev_count, off) != 0)
+          rc = fail("write %s failed", chunk_file);
+      }
     }
   }
 out:
   scratch_free(&S);
+  for (int k = 0; k < 2; ++k) {
+    if (ev_recv[k]) (void) hipEventDestroy(ev_recv[k]);
+    if (ev_par[k]) (void) hipEventDestroy(ev_par[k]);
+  }
   free(mat);
   free(coef);
   free(ins);
@@ -279,6 +335,9 @@ out:
 }
 
 /* ---- RS decode (replaces redset_reedsolomon_decode, src/redset_reedsolomon.c:570-785) */
+
+#define TAG_RING 0
+#define TAG_GATHER 1
 
 int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missing, const int* rebuild_ranks,
                               int need_rebuild, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
@@ -289,8 +348,6 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   if (comm_geometry(comm, &p, &r) || redset_hip_rs_shape(rs, &rp, &e)) return REDSET_FAILURE;
   if (p != rp) return fail("communicator has %d ranks, codec %d", p, rp);
   if (missing < 1 || missing > e) return fail("cannot rebuild %d members with %d encoding blocks", missing, e);
-  /* a bad fd on one member is agreed on below, not returned early: its
-   * peers would wait for it in the first collective */
   const int hrc = header_size(fd_chunk, chunk_file, &header);
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
 
@@ -302,13 +359,18 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   MPI_Request* req = malloc(sizeof(*req) * (size_t) (2 * p + missing + 2));
   scratch S;
   scratch_init(&S);
+  /* two sets of slice buffers: slice n's ring exchange and GPU solve overlap
+   * slice n-1's gather to the erased members and its writes */
   uint8_t* h_send = scratch_host(&S, B);
-  uint8_t* h_cells = scratch_host(&S, (size_t) p * B);  /* member s's cell of stripe r */
-  uint8_t* h_out = scratch_host(&S, (size_t) missing * B);
+  uint8_t* h_cells[2] = {scratch_host(&S, (size_t) p * B), scratch_host(&S, (size_t) p * B)};
+  uint8_t* h_out[2] = {scratch_host(&S, (size_t) missing * B), scratch_host(&S, (size_t) missing * B)};
   uint8_t* h_gather = scratch_host(&S, (size_t) p * B); /* rebuilt cells from every solver */
-  uint8_t* d_cells = scratch_dev(&S, (size_t) p * B);
-  uint8_t* d_out = scratch_dev(&S, (size_t) missing * B);
+  uint8_t* d_cells[2] = {scratch_dev(&S, (size_t) p * B), scratch_dev(&S, (size_t) p * B)};
+  uint8_t* d_out[2] = {scratch_dev(&S, (size_t) missing * B), scratch_dev(&S, (size_t) missing * B)};
+  hipEvent_t ev_done[2] = {NULL, NULL};
   int rc = S.rc ? S.rc : hrc;
+  for (int k = 0; k < 2 && !rc; ++k)
+    if (hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
   if (!rc && (!D || !coef || !cols || !ins || !outs || !req)) rc = fail("out of host memory");
   /* member r solves stripe r (decode_chunk_id = rank, :607-611): one linear
    * map equal to redset_rs_reduce_decode + redset_rs_gaussian_solve */
@@ -322,82 +384,104 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   }
   for (int i = 0; i < missing; ++i)
     for (int k = 0; k < ncols; ++k) coef[(size_t) i * ncols + k] = D[(size_t) i * p + cols[k]];
-  for (int k = 0; k < ncols; ++k) ins[k] = d_cells + (size_t) cols[k] * B;
-  for (int i = 0; i < missing; ++i) outs[i] = d_out + (size_t) i * B;
 
   /* after a device failure every MPI call of the loop still runs (peers must
    * not hang, src/redset_reedsolomon.c:666-681 keep going on read errors);
    * this member then sends zeros as its solved cells and fails the call */
   int dev_failed = 0;
-  for (size_t nread = 0; nread < chunk_size; nread += B) {
-    const size_t count = min_sz(B, chunk_size - nread);
-    for (int step = 0; step < p; ++step) { /* :646-703 */
-      const int lhs = (r - step + p) % p, rhs = (r + step) % p;
-      const int chunk_id = (r + step) % p;
-      const int enc = redset_hip_rs_get_encoding_id(p, e, r, chunk_id);
-      if (!need_rebuild) {
-        int bad;
-        if (enc < p) {
-          const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
-          bad = lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0;
-          if (bad) rc = fail("lofi read failed");
+  int have_prev = 0, prev_b = 0;
+  size_t prev_nread = 0, prev_count = 0;
+  size_t n = 0;
+  for (size_t nread = 0;; nread += B, ++n) {
+    const int more = nread < chunk_size;
+    const size_t count = more ? min_sz(B, chunk_size - nread) : 0;
+    const int bb = (int) (n & 1);
+    if (more) {
+      for (int step = 0; step < p; ++step) { /* :646-703 */
+        const int lhs = (r - step + p) % p, rhs = (r + step) % p;
+        const int chunk_id = (r + step) % p;
+        const int enc = redset_hip_rs_get_encoding_id(p, e, r, chunk_id);
+        if (!need_rebuild) {
+          int bad;
+          if (enc < p) {
+            const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
+            bad = lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0;
+            if (bad) rc = fail("lofi read failed");
+          } else {
+            const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) nread;
+            bad = pread_full(fd_chunk, h_send, count, off) != 0;
+            if (bad) rc = fail("read %s failed", chunk_file);
+          }
+          if (bad) memset(h_send, 0, count);
         } else {
-          const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) nread;
-          bad = pread_full(fd_chunk, h_send, count, off) != 0;
-          if (bad) rc = fail("read %s failed", chunk_file);
+          memset(h_send, 0, count); /* an erased member contributes nothing */
         }
-        if (bad) memset(h_send, 0, count);
-      } else {
-        memset(h_send, 0, count); /* an erased member contributes nothing */
+        if (step > 0) {
+          MPI_Irecv(h_cells[bb] + (size_t) lhs * B, (int) count, MPI_BYTE, lhs, TAG_RING, comm, &req[0]);
+          MPI_Isend(h_send, (int) count, MPI_BYTE, rhs, TAG_RING, comm, &req[1]);
+          MPI_Waitall(2, req, MPI_STATUSES_IGNORE);
+        } else {
+          memcpy(h_cells[bb] + (size_t) r * B, h_send, count);
+        }
       }
-      if (step > 0) {
-        MPI_Irecv(h_cells + (size_t) lhs * B, (int) count, MPI_BYTE, lhs, 0, comm, &req[0]);
-        MPI_Isend(h_send, (int) count, MPI_BYTE, rhs, 0, comm, &req[1]);
-        MPI_Waitall(2, req, MPI_STATUSES_IGNORE);
-      } else {
-        memcpy(h_cells + (size_t) r * B, h_send, count);
+      /* enqueue this slice's solve; it runs while the previous slice is gathered */
+      if (!dev_failed) {
+        for (int k = 0; k < ncols; ++k) ins[k] = d_cells[bb] + (size_t) cols[k] * B;
+        for (int i = 0; i < missing; ++i) outs[i] = d_out[bb] + (size_t) i * B;
+        int grc = injected_device_failure(comm);
+        if (!grc) grc = h2d(&S, d_cells[bb], h_cells[bb], (size_t) p * B);
+        if (!grc && ncols > 0) grc = redset_hip_gf_combine(ins, ncols, outs, missing, coef, count, 0, S.stream);
+        if (!grc) grc = d2h(&S, h_out[bb], d_out[bb], (size_t) missing * B);
+        if (!grc) grc = ev_record(&S, ev_done[bb]);
+        if (grc) {
+          rc = grc;
+          dev_failed = 1;
+        }
       }
     }
-    if (!dev_failed) {
-      int grc = injected_device_failure(comm);
-      if (!grc) grc = h2d(&S, d_cells, h_cells, (size_t) p * B);
-      if (!grc && ncols > 0) grc = redset_hip_gf_combine(ins, ncols, outs, missing, coef, count, 0, S.stream);
-      if (!grc) grc = d2h(&S, h_out, d_out, (size_t) missing * B);
-      if (!grc) grc = sync_stream(&S);
-      if (grc) {
-        rc = grc;
+    if (have_prev) {
+      /* previous slice: its solved cells to the erased members, :713-733 */
+      if (!dev_failed && ev_wait(ev_done[prev_b])) {
+        rc = REDSET_FAILURE;
         dev_failed = 1;
       }
-    }
-    if (dev_failed) memset(h_out, 0, (size_t) missing * B);
-    /* gather rebuilt cells to the erased members, :713-733 */
-    int k = 0;
-    if (need_rebuild)
-      for (int step = 0; step < p; ++step) {
-        const int lhs = (r - step + p) % p;
-        MPI_Irecv(h_gather + (size_t) lhs * B, (int) count, MPI_BYTE, lhs, 0, comm, &req[k++]);
-      }
-    for (int i = 0; i < missing; ++i)
-      MPI_Isend(h_out + (size_t) i * B, (int) count, MPI_BYTE, rebuild_ranks[i], 0, comm, &req[k++]);
-    MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
-    if (need_rebuild) { /* :736-765 */
-      for (int step = 0; step < p; ++step) {
-        const int lhs = (r - step + p) % p;
-        const int enc = redset_hip_rs_get_encoding_id(p, e, r, lhs);
-        const uint8_t* cell = h_gather + (size_t) lhs * B;
-        if (enc < p) {
-          const int seg = redset_hip_rs_get_data_id(p, e, r, lhs);
-          if (!lofi->write || lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, cell) != 0)
-            rc = fail("lofi write failed");
-        } else {
-          const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) nread;
-          if (pwrite_full(fd_chunk, cell, count, off) != 0) rc = fail("write %s failed", chunk_file);
+      if (dev_failed) memset(h_out[prev_b], 0, (size_t) missing * B);
+      int k = 0;
+      if (need_rebuild)
+        for (int step = 0; step < p; ++step) {
+          const int lhs = (r - step + p) % p;
+          MPI_Irecv(h_gather + (size_t) lhs * B, (int) prev_count, MPI_BYTE, lhs, TAG_GATHER, comm, &req[k++]);
+        }
+      for (int i = 0; i < missing; ++i)
+        MPI_Isend(h_out[prev_b] + (size_t) i * B, (int) prev_count, MPI_BYTE, rebuild_ranks[i], TAG_GATHER, comm,
+                  &req[k++]);
+      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+      if (need_rebuild) { /* :736-765 */
+        for (int step = 0; step < p; ++step) {
+          const int lhs = (r - step + p) % p;
+          const int enc = redset_hip_rs_get_encoding_id(p, e, r, lhs);
+          const uint8_t* cell = h_gather + (size_t) lhs * B;
+          if (enc < p) {
+            const int seg = redset_hip_rs_get_data_id(p, e, r, lhs);
+            if (!lofi->write || lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, prev_nread, prev_count, cell) != 0)
+              rc = fail("lofi write failed");
+          } else {
+            const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) prev_nread;
+            if (pwrite_full(fd_chunk, cell, prev_count, off) != 0) rc = fail("write %s failed", chunk_file);
+          }
         }
       }
     }
+    if (!more) break;
+    have_prev = 1;
+    prev_b = bb;
+    prev_nread = nread;
+    prev_count = count;
   }
 out:
   scratch_free(&S);
+  for (int k = 0; k < 2; ++k)
+    if (ev_done[k]) (void) hipEventDestroy(ev_done[k]);
   free(D);
   free(coef);
   free(cols);
@@ -425,50 +509,77 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
   MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) p);
   scratch S;
   scratch_init(&S);
+  /* two sets of receive / result buffers: slice n's exchange runs while the
+   * GPU combines slice n-1, whose result is written after it */
   uint8_t* h_send = scratch_host(&S, (size_t) p * B); /* my cell of stripe t, for t != r */
-  uint8_t* h_recv = scratch_host(&S, (size_t) p * B); /* member t's cell of stripe r */
-  uint8_t* h_out = scratch_host(&S, B);
-  uint8_t* d_recv = scratch_dev(&S, (size_t) p * B);
-  uint8_t* d_out = scratch_dev(&S, B);
+  uint8_t* h_recv[2] = {scratch_host(&S, (size_t) p * B), scratch_host(&S, (size_t) p * B)};
+  uint8_t* h_out[2] = {scratch_host(&S, B), scratch_host(&S, B)};
+  uint8_t* d_recv[2] = {scratch_dev(&S, (size_t) p * B), scratch_dev(&S, (size_t) p * B)};
+  uint8_t* d_out[2] = {scratch_dev(&S, B), scratch_dev(&S, B)};
+  hipEvent_t ev_done[2] = {NULL, NULL};
   int rc = S.rc ? S.rc : hrc;
+  for (int k = 0; k < 2 && !rc; ++k)
+    if (hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
   if (!rc && (!ins || !req)) rc = fail("out of host memory");
   if ((rc = agree_setup(comm, rc))) goto out;
-  int nin = 0;
-  for (int t = 0; t < p; ++t)
-    if (t != r) ins[nin++] = d_recv + (size_t) t * B;
   int dev_failed = 0; /* then keep exchanging, skip GPU work and writes */
+  int have_prev = 0, prev_b = 0;
+  size_t prev_nread = 0, prev_count = 0, n = 0;
 
-  for (size_t nread = 0; nread < chunk_size; nread += B) {
-    const size_t count = min_sz(B, chunk_size - nread);
-    int k = 0;
-    /* the ring of src/redset_xor.c:251-285 leaves member r with the XOR of
-     * every other member's cell of stripe r; exchange those cells directly */
-    for (int t = 0; t < p; ++t) {
-      if (t == r) continue;
-      if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, t), nread, count, h_send + (size_t) t * B) != 0) {
-        rc = fail("lofi read failed");
-        memset(h_send + (size_t) t * B, 0, count);
+  for (size_t nread = 0;; nread += B, ++n) {
+    const int more = nread < chunk_size;
+    const size_t count = more ? min_sz(B, chunk_size - nread) : 0;
+    const int bb = (int) (n & 1);
+    if (more) {
+      /* the copy that read this receive buffer (slice n-2) is done: waited
+       * for below when slice n-2's result was written */
+      int k = 0;
+      /* the ring of src/redset_xor.c:251-285 leaves member r with the XOR of
+       * every other member's cell of stripe r; exchange those cells directly */
+      for (int t = 0; t < p; ++t) {
+        if (t == r) continue;
+        if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, t), nread, count,
+                       h_send + (size_t) t * B) != 0) {
+          rc = fail("lofi read failed");
+          memset(h_send + (size_t) t * B, 0, count);
+        }
+        MPI_Irecv(h_recv[bb] + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
+        MPI_Isend(h_send + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
       }
-      MPI_Irecv(h_recv + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
-      MPI_Isend(h_send + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
+      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+      if (!dev_failed) {
+        int nin = 0;
+        for (int t = 0; t < p; ++t)
+          if (t != r) ins[nin++] = d_recv[bb] + (size_t) t * B;
+        int grc = injected_device_failure(comm);
+        if (!grc) grc = h2d(&S, d_recv[bb], h_recv[bb], (size_t) p * B);
+        if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out[bb], count, 0, S.stream);
+        if (!grc) grc = d2h(&S, h_out[bb], d_out[bb], count);
+        if (!grc) grc = ev_record(&S, ev_done[bb]);
+        if (grc) {
+          rc = grc;
+          dev_failed = 1;
+        }
+      }
     }
-    MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
-    if (dev_failed) continue;
-    int grc = injected_device_failure(comm);
-    if (!grc) grc = h2d(&S, d_recv, h_recv, (size_t) p * B);
-    if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out, count, 0, S.stream);
-    if (!grc) grc = d2h(&S, h_out, d_out, count);
-    if (!grc) grc = sync_stream(&S);
-    if (grc) {
-      rc = grc;
-      dev_failed = 1;
-      continue;
+    if (have_prev && !dev_failed) {
+      if (ev_wait(ev_done[prev_b])) {
+        rc = REDSET_FAILURE;
+        dev_failed = 1;
+      } else if (pwrite_full(fd_chunk, h_out[prev_b], prev_count, header + (off_t) prev_nread) != 0) { /* :280-284 */
+        rc = fail("write %s failed", chunk_file);
+      }
     }
-    if (pwrite_full(fd_chunk, h_out, count, header + (off_t) nread) != 0) /* :280-284 */
-      rc = fail("write %s failed", chunk_file);
+    if (!more) break;
+    have_prev = 1;
+    prev_b = bb;
+    prev_nread = nread;
+    prev_count = count;
   }
 out:
   scratch_free(&S);
+  for (int k = 0; k < 2; ++k)
+    if (ev_done[k]) (void) hipEventDestroy(ev_done[k]);
   free(ins);
   free(req);
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;

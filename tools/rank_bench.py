@@ -20,6 +20,7 @@ MIB = 1 << 20
 
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--scheme", choices=["rs", "xor"], default="rs")
     ap.add_argument("--ranks", type=int, default=11)
     ap.add_argument("--encoding", type=int, default=3)
     ap.add_argument("--chunk-mib", type=int, default=16)
@@ -27,9 +28,9 @@ def main():
     ap.add_argument("--lost", default="1,2")
     ap.add_argument("--dir", default="/tmp/rank_bench")
     a = ap.parse_args()
-    p, e = a.ranks, a.encoding
+    p, e = a.ranks, (a.encoding if a.scheme == "rs" else 1)
     d, C = p - e, a.chunk_mib * MIB
-    lost = [int(x) for x in a.lost.split(",")]
+    lost = [int(x) for x in a.lost.split(",")][: 1 if a.scheme == "xor" else None]
     shutil.rmtree(a.dir, ignore_errors=True)
     os.makedirs(a.dir)
     block = np.frombuffer(np.random.default_rng(1).bytes(16 * MIB), np.uint8)
@@ -39,7 +40,7 @@ def main():
             for k in range(d * C // block.size):
                 f.write(np.roll(block, r * 131 + k).tobytes())
         with open(os.path.join(a.dir, f"manifest_{r}.txt"), "w") as f:
-            f.write(f"1\n{path} {d * C}\n{C}\n4096\n{os.path.join(a.dir, f'r{r}.rs.redset')}\n")
+            f.write(f"1\n{path} {d * C}\n{C}\n4096\n{os.path.join(a.dir, f'r{r}.{a.scheme}.redset')}\n")
     drv = os.path.join(ROOT, "tests", "mpi", "build", "rank_test")
     buf = int(a.buf_mib * MIB)
     out = {}
@@ -47,8 +48,8 @@ def main():
         if op == "rebuild":
             for r in lost:
                 os.unlink(os.path.join(a.dir, f"r{r}.dat"))
-                os.unlink(os.path.join(a.dir, f"r{r}.rs.redset"))
-        cmd = ["/opt/conda/bin/mpirun", "-np", str(p), "-host", "localhost", drv, "rs", op, str(e), a.dir, str(buf)] + \
+                os.unlink(os.path.join(a.dir, f"r{r}.{a.scheme}.redset"))
+        cmd = ["/opt/conda/bin/mpirun", "-np", str(p), "-host", "localhost", drv, a.scheme, op, str(e), a.dir, str(buf)] + \
             [str(x) for x in extra]
         res = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
         if res.returncode != 0:
@@ -57,7 +58,7 @@ def main():
         alg = p * (d + (e if op == "encode" else len(lost))) * C
         out[op] = {"seconds": t, "GBps": round(alg / t / 1e9, 3)}
     shutil.rmtree(a.dir, ignore_errors=True)
-    print(json.dumps({"ranks": p, "encoding": e, "chunk": C, "buf": buf, **out}))
+    print(json.dumps({"scheme": a.scheme, "ranks": p, "encoding": e, "chunk": C, "buf": buf, **out}))
 
 
 if __name__ == "__main__":

@@ -20,7 +20,12 @@ sys.path.insert(0, ROOT)
 MIB = 1 << 20
 
 
-def host_case(p, e, chunk, lost, slice_bytes, threads, pinned=True):
+def host_case(p, e, chunk, lost, slice_bytes, threads, mode="zero copy"):
+    """mode: "zero copy" (kernels read/write the page-locked cells over PCIe),
+    "direct DMA" (staged pipeline, SDMA straight from/to the page-locked cells)
+    or "staged" (read/write callbacks through pinned staging buffers)."""
+    pinned = mode != "staged"
+    os.environ["REDSET_HIP_ZERO_COPY"] = "1" if mode == "zero copy" else "0"
     import torch
     import redset_amd
     from redset_amd import stream
@@ -44,7 +49,7 @@ def host_case(p, e, chunk, lost, slice_bytes, threads, pinned=True):
     out = []
     enc = stream.rs_encode_stream(codec, chunk, io, slice_bytes=slice_bytes, io_threads=threads)
     alg = p * (d + e) * chunk
-    out.append({"case": "host encode" + (" (direct DMA)" if pinned else " (staged)"), "ranks": p, "encoding": e, "chunk": chunk, "GBps": alg / enc["seconds"] / 1e9,
+    out.append({"case": f"host encode ({mode})", "ranks": p, "encoding": e, "chunk": chunk, "GBps": alg / enc["seconds"] / 1e9,
                 "stats": enc, "setup_s": setup})
     # the lost members' regions (data + parity cells) are what the rebuild
     # must restore: snapshot them, erase, rebuild, compare
@@ -54,7 +59,7 @@ def host_case(p, e, chunk, lost, slice_bytes, threads, pinned=True):
     reb = stream.rs_rebuild_stream(codec, lost, chunk, io, slice_bytes=slice_bytes, io_threads=threads)
     alg_r = p * (d + len(lost)) * chunk
     ok = all(bool(torch.equal(buf[r * per:(r + 1) * per], x)) for r, x in zip(lost, ref))
-    out.append({"case": "host rebuild" + (" (direct DMA)" if pinned else " (staged)"), "ranks": p, "encoding": e,
+    out.append({"case": f"host rebuild ({mode})", "ranks": p, "encoding": e,
                 "chunk": chunk, "lost": lost, "GBps": alg_r / reb["seconds"] / 1e9, "stats": reb,
                 "round_trip_equal": ok})
     return out
@@ -266,13 +271,9 @@ def main():
     lost = [int(x) for x in a.lost.split(",")]
     res = []
     if a.mode in ("host", "both"):
-        res += host_case(a.ranks, a.encoding, a.chunk_mib * MIB, lost, a.slice_mib * MIB, a.threads, pinned=True)
-        for r in res:
-            print(json.dumps(r), flush=True)
-        res = host_case(a.ranks, a.encoding, a.chunk_mib * MIB, lost, a.slice_mib * MIB, a.threads, pinned=False)
-        for r in res:
-            print(json.dumps(r), flush=True)
-        res = []
+        for mode in ("zero copy", "direct DMA", "staged"):
+            for r in host_case(a.ranks, a.encoding, a.chunk_mib * MIB, lost, a.slice_mib * MIB, a.threads, mode):
+                print(json.dumps(r), flush=True)
     if a.mode in ("disk", "both"):
         out, files, reds, headers = disk_case(a.ranks, a.encoding, a.disk_chunk_mib * MIB, lost, a.slice_mib * MIB,
                                               a.threads, a.dir, a.short_mib, bool(a.cold))

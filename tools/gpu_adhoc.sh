@@ -1,7 +1,14 @@
 set -o pipefail
 cd "${GRAFT_REPO_ROOT}"
 export TMPDIR=/tmp
-OUT=gpurun_out/r02s15
+OUT=gpurun_out/r02s17
 mkdir -p $OUT
-timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread -m gpu tests/test_gpu_stream.py tests/test_gpu_setfiles.py > $OUT/tests.log 2>&1; s=$?; tail -3 $OUT/tests.log; [ $s -eq 0 ] || exit $s
-timeout -k 10 900 python -u tools/bench_e2e.py --mode host > $OUT/e2e.jsonl 2> $OUT/e2e.err; s=$?; cut -c1-330 $OUT/e2e.jsonl; exit $s
+for od in 1 0; do
+  for cfg in "--slice-mib 8 --threads 16" "--slice-mib 32 --threads 16"; do
+    REDSET_HIP_ODIRECT=$od timeout -k 10 600 python -u tools/bench_e2e.py --mode disk --cpu-stripes "" $cfg > $OUT/e.tmp 2> $OUT/e.err || exit $?
+    python3 -c "
+import json
+for l in open('$OUT/e.tmp'):
+    d=json.loads(l); print(json.dumps({'odirect': $od, 'cfg': '$cfg', 'case': d['case'], 'GBps': round(d['GBps'],2), 'rt': d.get('round_trip_equal')}))" | tee -a $OUT/sweep.jsonl
+  done
+done

@@ -451,3 +451,34 @@ def test_sharded_runner_world1_hip(rd, oracle):
     torch.cuda.synchronize()
     assert np.array_equal(run.D_host.cpu().numpy()[..., :chunk], data[..., :chunk])
     assert np.array_equal(run.P_host.cpu().numpy()[..., :chunk], par[..., :chunk])
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_random_shapes_encode_rebuild(rd, oracle, case):
+    """Seeded random set shapes (p up to 60, e up to 8, odd chunks, packed or
+    padded cells): GPU encode and rebuild plans against the oracle."""
+    rng = np.random.default_rng(1000 + case)
+    p = int(rng.integers(2, 61))
+    e = int(rng.integers(1, min(p - 1, 8) + 1))
+    chunk = int(rng.integers(1, 5000))
+    padded = bool(rng.integers(0, 2))
+    lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=case)
+    lay = upload_set(rd, lofi, parity, p - e, e, chunk, padded=padded)
+    codec = rd.RSCodec(p, e)
+    codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride).execute()
+    torch.cuda.synchronize()
+    st = oracle.OracleRS(p, e)
+    st.encode_set(lofi, parity, chunk)
+    _, got = download_set(lay)
+    for r in range(p):
+        assert np.array_equal(got[r], parity[r]), (p, e, chunk, r)
+    m = int(rng.integers(1, e + 1))
+    lost = sorted(rng.choice(p, size=m, replace=False).tolist())
+    for r in lost:
+        lay.lofi(r).fill_(0xEE)
+        lay.parity(r).fill_(0xEE)
+    codec.plan_rebuild(lost, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride).execute()
+    torch.cuda.synchronize()
+    gl, gp = download_set(lay)
+    for r in range(p):
+        assert np.array_equal(gl[r], lofi[r]) and np.array_equal(gp[r], parity[r]), (p, e, chunk, lost, r)

@@ -94,9 +94,6 @@ static int d2h(scratch* S, void* dst, const void* src, size_t n) {
   return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, S->stream) == hipSuccess ? 0 : fail("D2H copy failed");
 }
 
-static int sync_stream(scratch* S) {
-  return hipStreamSynchronize(S->stream) == hipSuccess ? 0 : fail("hipStreamSynchronize failed");
-}
 
 /* ---- file I/O: full pread / pwrite (redset_read_attempt /
  * redset_write_attempt, src/redset_io.c:234-310) --------------------------- */
@@ -603,26 +600,33 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   MPI_Request* req = malloc(sizeof(*req) * (size_t) p);
   scratch S;
   scratch_init(&S);
-  uint8_t* h_cells = scratch_host(&S, (size_t) p * B);
-  uint8_t* h_out = scratch_host(&S, B);
-  uint8_t* d_cells = scratch_dev(&S, (size_t) p * B);
-  uint8_t* d_out = scratch_dev(&S, B);
+  /* the root double-buffers: unit n's cells arrive while the GPU XORs unit
+   * n-1, whose result is written after */
+  uint8_t* h_cells[2] = {scratch_host(&S, (size_t) p * B), scratch_host(&S, (size_t) p * B)};
+  uint8_t* h_out[2] = {scratch_host(&S, B), scratch_host(&S, B)};
+  uint8_t* d_cells[2] = {scratch_dev(&S, (size_t) p * B), scratch_dev(&S, (size_t) p * B)};
+  uint8_t* d_out[2] = {scratch_dev(&S, B), scratch_dev(&S, B)};
+  hipEvent_t ev_done[2] = {NULL, NULL};
   int rc = S.rc ? S.rc : hrc;
+  for (int k = 0; k < 2 && !rc; ++k)
+    if (hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
   if (!rc && (!ins || !req)) rc = fail("out of host memory");
   if ((rc = agree_setup(comm, rc))) goto out;
-  int nin = 0;
-  for (int t = 0; t < p; ++t)
-    if (t != root) ins[nin++] = d_cells + (size_t) t * B;
   int dev_failed = 0; /* root: keep receiving every cell, skip GPU work and writes */
+  int have_prev = 0, prev_b = 0, prev_c = 0;
+  size_t prev_nread = 0, prev_count = 0;
+  long n = 0;
 
   /* stripe by stripe, as the reference's pipelined reduce to the root
    * (src/redset_xor.c:466-524): every survivor sends its cell of stripe c,
    * the root XORs them on the GPU and writes its own cell of stripe c */
-  for (int c = 0; c < p; ++c) {
-    for (size_t nread = 0; nread < chunk_size; nread += B) {
-      const size_t count = min_sz(B, chunk_size - nread);
-      if (r != root) {
-        uint8_t* mine = h_cells + (size_t) r * B;
+  for (int c = 0; c <= p; ++c) {
+    for (size_t nread = 0; c == p ? nread == 0 : nread < chunk_size; nread += B, ++n) {
+      const int more = c < p;  /* c == p: one last pass to write the final unit */
+      const size_t count = more ? min_sz(B, chunk_size - nread) : 0;
+      const int bb = (int) (n & 1);
+      if (more && r != root) {
+        uint8_t* mine = h_cells[0] + (size_t) r * B;
         int bad;
         if (c != r) {
           bad = lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, c), nread, count, mine) != 0;
@@ -635,32 +639,52 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
         MPI_Send(mine, (int) count, MPI_BYTE, root, 0, comm);
         continue;
       }
-      int k = 0;
-      for (int t = 0; t < p; ++t)
-        if (t != root) MPI_Irecv(h_cells + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
-      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
-      if (dev_failed) continue;
-      int grc = injected_device_failure(comm);
-      if (!grc) grc = h2d(&S, d_cells, h_cells, (size_t) p * B);
-      if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out, count, 0, S.stream);
-      if (!grc) grc = d2h(&S, h_out, d_out, count);
-      if (!grc) grc = sync_stream(&S);
-      if (grc) {
-        rc = grc;
-        dev_failed = 1;
-        continue;
+      if (r != root) continue;
+      if (more) {
+        /* h_cells[bb] was last read by unit n-2's copy, waited for when
+         * unit n-2 was written (below, during unit n-1) */
+        int k = 0;
+        for (int t = 0; t < p; ++t)
+          if (t != root) MPI_Irecv(h_cells[bb] + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
+        MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+        if (!dev_failed) {
+          int nin = 0;
+          for (int t = 0; t < p; ++t)
+            if (t != root) ins[nin++] = d_cells[bb] + (size_t) t * B;
+          int grc = injected_device_failure(comm);
+          if (!grc) grc = h2d(&S, d_cells[bb], h_cells[bb], (size_t) p * B);
+          if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out[bb], count, 0, S.stream);
+          if (!grc) grc = d2h(&S, h_out[bb], d_out[bb], count);
+          if (!grc) grc = ev_record(&S, ev_done[bb]);
+          if (grc) {
+            rc = grc;
+            dev_failed = 1;
+          }
+        }
       }
-      if (c != root) {
-        if (!lofi->write ||
-            lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(root, c), nread, count, h_out) != 0)
-          rc = fail("lofi write failed");
-      } else if (pwrite_full(fd_chunk, h_out, count, header + (off_t) nread) != 0) {
-        rc = fail("write %s failed", chunk_file);
+      if (have_prev && !dev_failed) {
+        if (ev_wait(ev_done[prev_b])) {
+          rc = REDSET_FAILURE;
+          dev_failed = 1;
+        } else if (prev_c != root) {
+          if (!lofi->write || lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(root, prev_c), prev_nread,
+                                          prev_count, h_out[prev_b]) != 0)
+            rc = fail("lofi write failed");
+        } else if (pwrite_full(fd_chunk, h_out[prev_b], prev_count, header + (off_t) prev_nread) != 0) {
+          rc = fail("write %s failed", chunk_file);
+        }
       }
+      have_prev = more;
+      prev_b = bb;
+      prev_c = c;
+      prev_nread = nread;
+      prev_count = count;
     }
   }
 out:
   scratch_free(&S);
+  for (int k = 0; k < 2; ++k)
+    if (ev_done[k]) (void) hipEventDestroy(ev_done[k]);
   free(ins);
   free(req);
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;

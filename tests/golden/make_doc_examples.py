@@ -20,6 +20,11 @@ product library is used here, so these fixtures pin both of them.
   row. With the figure's placement:
       c0 (row 0) = 28 * seg(1, 0) + 18 * seg(2, 0)
       c1 (row 1) = 20 * seg(2, 1) + 18 * seg(3, 0)
+* XOR, doc/rst/fig/xor.png (schemes.rst:185-200, "Logically insert alternating
+  zero-padded chunk and reduce"; "Scatter XOR chunks among the different
+  ranks"): with N = 4 processes each logical file splits into N-1 chunks,
+  process r's column has a zero PAD chunk at row r, and XOR:c -- the XOR of
+  row c over all processes -- is stored by process c (XOR_FIGURE_COLUMNS).
 * Rebuild, doc/rst/schemes.rst:650-693: processes 1 and 2 lost, second row
   of chunks. Unknowns x = (d2, c0), d2 = seg(2, 1), c0 = process 1's first
   checksum chunk; A = [[18, 1], [20, 0]], b = (20*d3, 18*d3 + c1) with
@@ -39,6 +44,15 @@ FIGURE_COLUMNS = [
     ["1:0", "C0", "C1", "1:1"],
     ["2:0", "2:1", "C0", "C1"],
     ["C1", "3:0", "3:1", "C0"],
+]
+
+
+# doc/rst/fig/xor.png, middle panel: XOR_FIGURE_COLUMNS[process][row]
+XOR_FIGURE_COLUMNS = [
+    ["PAD", "0:0", "0:1", "0:2"],
+    ["1:0", "PAD", "1:1", "1:2"],
+    ["2:0", "2:1", "PAD", "2:2"],
+    ["3:0", "3:1", "3:2", "PAD"],
 ]
 
 
@@ -105,7 +119,18 @@ def main():
     np.savez_compressed(os.path.join(HERE, "doc_p4_e2_rebuild.npz"), ranks=4, encoding=2, chunk=CHUNK,
                         lost=np.array([1, 2]), row=1, A=A, d3=d3, c1=c1, b=np.stack([b0, b1]),
                         d2=d2, c0=c0_row1, map_known_d3_c1=D)
-    print("wrote doc_p4_e2_encode.npz, doc_p4_e2_rebuild.npz")
+    # XOR set of the figure: 4 processes, 3 chunks each
+    xlofi = rng.integers(0, 256, size=(4, 3 * CHUNK), dtype=np.uint8)
+    xseg = lambda s, j: xlofi[s, j * CHUNK:(j + 1) * CHUNK]  # noqa: E731
+    xor_cells = np.zeros((4, CHUNK), np.uint8)
+    for row in range(4):
+        for s in range(4):
+            label = XOR_FIGURE_COLUMNS[s][row]
+            if label != "PAD":
+                xor_cells[row] ^= xseg(*map(int, label.split(":")))
+    np.savez_compressed(os.path.join(HERE, "doc_xor_p4.npz"), ranks=4, chunk=CHUNK, lofi=xlofi,
+                        xor_of_process=xor_cells, figure_columns=np.array(XOR_FIGURE_COLUMNS))
+    print("wrote doc_p4_e2_encode.npz, doc_p4_e2_rebuild.npz, doc_xor_p4.npz")
 
 
 if __name__ == "__main__":

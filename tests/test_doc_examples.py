@@ -172,3 +172,63 @@ def test_gpu_encode_and_rebuild_match_documented_examples():
         for r in range(P):
             assert np.array_equal(lay.lofi(r).cpu().numpy().reshape(P - E, -1)[:, :C].reshape(-1),
                                   ENC["lofi"][r]), (padded, r)
+
+
+# --------------------------------------------------------------------------
+# XOR: doc/rst/fig/xor.png (4 processes, PAD at row r of process r, XOR:c on
+# process c)
+# --------------------------------------------------------------------------
+
+XOR = _load("doc_xor_p4.npz")
+XC = int(XOR["chunk"])
+
+
+def test_xor_figure_layout_is_the_reference_rule():
+    """The figure's columns follow src/redset_xor.c:251-266: process t's
+    chunk in row c is segment c for c < t and c - 1 for c > t."""
+    fig = [[str(x) for x in row] for row in XOR["figure_columns"]]
+    for t in range(4):
+        for c in range(4):
+            want = "PAD" if c == t else f"{t}:{c if c < t else c - 1}"
+            assert fig[t][c] == want
+
+
+def test_oracle_xor_encode_and_rebuild_match_figure(oracle):
+    lofi = [XOR["lofi"][r].copy() for r in range(4)]
+    xorc = [np.zeros(XC, np.uint8) for _ in range(4)]
+    oracle.xor_encode_set(4, lofi, xorc, XC)
+    for r in range(4):
+        assert np.array_equal(xorc[r], XOR["xor_of_process"][r]), r
+    for root in range(4):
+        lf = [x.copy() for x in lofi]
+        xc = [x.copy() for x in xorc]
+        lf[root][:] = 0
+        xc[root][:] = 0
+        oracle.xor_rebuild_set(4, root, lf, xc, XC)
+        assert np.array_equal(lf[root], XOR["lofi"][root]) and np.array_equal(xc[root], XOR["xor_of_process"][root])
+
+
+@pytest.mark.gpu
+def test_gpu_xor_encode_and_rebuild_match_figure():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import redset_amd as rd
+
+    lay = rd.SetLayout.allocate(4, 3, 1, XC)
+    lay.storage.fill_(0x5A)
+    for r in range(4):
+        for s in range(3):
+            lay.data_cell(r, s).copy_(torch.from_numpy(XOR["lofi"][r][s * XC:(s + 1) * XC].copy()))
+    rd.xor_plan_encode(4, lay.lofi_ptrs(), lay.parity_ptrs(), XC, lay.cell_stride).execute()
+    torch.cuda.synchronize()
+    for r in range(4):
+        assert np.array_equal(lay.parity_cell(r, 0).cpu().numpy(), XOR["xor_of_process"][r]), r
+    for root in range(4):
+        lay.lofi(root).fill_(0xEE)
+        lay.parity(root).fill_(0xEE)
+        rd.xor_plan_rebuild(4, root, lay.lofi_ptrs(), lay.parity_ptrs(), XC, lay.cell_stride).execute()
+        torch.cuda.synchronize()
+        got = np.concatenate([lay.data_cell(root, s).cpu().numpy() for s in range(3)])
+        assert np.array_equal(got, XOR["lofi"][root]), root
+        assert np.array_equal(lay.parity_cell(root, 0).cpu().numpy(), XOR["xor_of_process"][root]), root

@@ -15,6 +15,7 @@
 #include "redset_hip_mpi.h"
 
 #include <errno.h>
+#include <limits.h>
 #include <hip/hip_runtime_api.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -188,6 +189,7 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
   const int hrc = header_size(fd_chunk, chunk_file, &header);
   const int d = p - e;
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
   /* ring steps staged per window: the d*e slices of a slice's whole ring
    * would need d*e*B of pinned and device memory (O(p*e)); windows of G steps
    * bound each staging buffer to MAX_STAGE, the reference's own scratch being
@@ -347,6 +349,7 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   if (missing < 1 || missing > e) return fail("cannot rebuild %d members with %d encoding blocks", missing, e);
   const int hrc = header_size(fd_chunk, chunk_file, &header);
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
 
   unsigned char* D = malloc((size_t) missing * p); /* decode map of stripe r: missing x p */
   unsigned char* coef = malloc((size_t) missing * p);
@@ -501,6 +504,7 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
    * peers would wait for it in the first collective */
   const int hrc = header_size(fd_chunk, chunk_file, &header);
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
 
   const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
   MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) p);
@@ -595,6 +599,7 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
    * peers would wait for it in the first collective */
   const int hrc = header_size(fd_chunk, chunk_file, &header);
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
 
   const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
   MPI_Request* req = malloc(sizeof(*req) * (size_t) p);

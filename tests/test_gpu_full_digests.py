@@ -66,3 +66,36 @@ def test_full_size_parity_digests(rd, name):
     for r in case["lost"]:
         assert full_size.sha256(cells(lay.lofi(r), d).cpu().numpy()) == want["lofi_sha256"][r], r
         assert full_size.sha256(cells(lay.parity(r), e).cpu().numpy()) == want["parity_sha256"][r], r
+
+
+def test_full_size_sharded_rebuild_digests(rd):
+    """BASELINE.json configs[3] (RS(8+3), erase 2 ranks, sharded rebuild) at
+    its 64 MiB chunks through the C sharded plan and the RCCL transport at
+    world size 1 (a one-rank communicator; the multi-GPU slicing is covered at
+    world 2-4 by tests/test_gpu_mpi.py and test_mpi_sharded.py). Same inputs
+    and oracle digests as configs[2]'s case above."""
+    from redset_amd.dist import ShardedSetRunner
+
+    case = full_size.CASES["rs_p11_e3_c64MiB"]
+    with open(DIGESTS) as f:
+        want = json.load(f)["rs_p11_e3_c64MiB"]
+    p, e, C = case["ranks"], case["encoding"], case["chunk"]
+    d = p - e
+    run = ShardedSetRunner(p, e, C, case["lost"], world=1, rank=0, fill=False)
+    try:
+        assert run.W == C
+        slot = [run.host_of(0, r)[1] for r in range(p)]
+        for r in range(p):
+            run.D_host[0, slot[r]].copy_(torch.from_numpy(full_size.member_lofi(case, r)).view(d, C))
+        run.encode()
+        torch.cuda.synchronize()
+        for r in range(p):
+            assert full_size.sha256(run.P_host[0, slot[r]].cpu().numpy()) == want["parity_sha256"][r], r
+        run.erase()
+        run.rebuild()
+        torch.cuda.synchronize()
+        for r in range(p):
+            assert full_size.sha256(run.D_host[0, slot[r]].cpu().numpy()) == want["lofi_sha256"][r], r
+            assert full_size.sha256(run.P_host[0, slot[r]].cpu().numpy()) == want["parity_sha256"][r], r
+    finally:
+        run.close()

@@ -169,3 +169,38 @@ def test_mpi_sharded_gpu(np_, p, e, chunk, lost):
     res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
     assert res.returncode == 0, res.stdout + res.stderr
     assert res.stdout.count("rebuild gather") == np_
+
+
+def test_mpi_config0_xor_4_ranks_16MiB(oracle, tmp_path):
+    """BASELINE.json configs[0] at its own shape through the drop-in per-rank
+    XOR backend: 4 MPI ranks, one 16 MiB file each (chunk = ceil(16 MiB / 3),
+    src/redset_xor.c's rule), 1 MiB MPI buffer; encode, lose rank 2, rebuild."""
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    tmp = str(tmp_path)
+    p, e, size = 4, 1, 16 << 20
+    rng = np.random.default_rng(0xC0)
+    files = []
+    for r in range(p):
+        path = os.path.join(tmp, f"r{r}.dat")
+        rng.integers(0, 256, size, dtype=np.uint8).tofile(path)
+        files.append([(path, size)])
+    chunk = -(-size // (p - 1))
+    header = [4096] * p
+    reds = [os.path.join(tmp, f"r{r}.xor.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, header, reds)
+    res = _mpirun(p, ["xor", "encode", e, tmp, 1 << 20])
+    assert res.returncode == 0, res.stdout + res.stderr
+    lofi = [_logical(fl, (p - 1) * chunk) for fl in files]
+    want = [np.zeros(chunk, np.uint8) for _ in range(p)]
+    oracle.xor_encode_set(p, lofi, want, chunk)
+    for r in range(p):
+        assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[4096:], want[r]), r
+    crc = oracle.crc32(lofi[2][:size])
+    os.unlink(files[2][0][0])
+    os.unlink(reds[2])
+    res = _mpirun(p, ["xor", "rebuild", e, tmp, 1 << 20, 2])
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert os.path.getsize(files[2][0][0]) == size
+    assert oracle.crc32(np.fromfile(files[2][0][0], dtype=np.uint8)) == crc
+    assert np.array_equal(np.fromfile(reds[2], dtype=np.uint8)[4096:], want[2])

@@ -29,6 +29,7 @@ def main():
     ap.add_argument("--buf-mib", type=float, default=1.0)
     ap.add_argument("--lost", default="1,2")
     ap.add_argument("--dir", default="/tmp/rank_bench")
+    ap.add_argument("--repeat", type=int, default=1, help="calls per process; the last one is reported as warm")
     a = ap.parse_args()
     p, e = a.ranks, (a.encoding if a.scheme == "rs" else 1)
     d = p - e
@@ -63,12 +64,17 @@ def main():
                 os.unlink(os.path.join(a.dir, f"r{r}.{a.scheme}.redset"))
         cmd = ["/opt/conda/bin/mpirun", "-np", str(p), "-host", "localhost", drv, a.scheme, op, str(e), a.dir, str(buf)] + \
             [str(x) for x in extra]
-        res = subprocess.run(cmd, capture_output=True, text=True, timeout=900)
+        res = subprocess.run(cmd, capture_output=True, text=True, timeout=900,
+                             env={**os.environ, "RANK_TEST_REPEAT": str(a.repeat)})
         if res.returncode != 0:
             raise SystemExit(res.stdout + res.stderr)
         t = float(re.search(r": ([0-9.]+) s", res.stdout).group(1))
         alg = p * (d + (e if op == "encode" else len(lost))) * C
         out[op] = {"seconds": t, "GBps": round(alg / t / 1e9, 3)}
+        warm = re.search(r"\(warm\): ([0-9.]+) s", res.stdout)
+        if warm:
+            tw = float(warm.group(1))
+            out[op].update(warm_seconds=tw, warm_GBps=round(alg / tw / 1e9, 3))
     for r in lost:  # the rebuilt files must be the originals
         with open(os.path.join(a.dir, f"r{r}.dat"), "rb") as f:
             if any(f.read(len(piece)) != piece for piece in content(r)) or f.read(1):

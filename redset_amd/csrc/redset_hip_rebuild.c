@@ -103,6 +103,9 @@ static int load_headers(int nfiles, char** files, int* ranks_out, int* rs_out, i
   member* m = NULL;
   htree* group = NULL;
   char kb[16];
+  /* the caller frees *m_out / *group_out (free_set) on success and failure alike */
+  *m_out = NULL;
+  *group_out = NULL;
   for (int i = 0; i < nfiles; ++i) {
     int fd = open(files[i], O_RDONLY);
     if (fd < 0) continue;
@@ -132,6 +135,9 @@ static int load_headers(int nfiles, char** files, int* ranks_out, int* rs_out, i
       enc = rs ? (int) k : 1;
       m = calloc((size_t) ranks, sizeof(member));
       group = ht_copy(g);
+      *ranks_out = ranks;
+      *m_out = m;
+      *group_out = group;
     }
     if (me >= (unsigned long long) ranks) {
       ht_free(h);
@@ -195,12 +201,20 @@ static int load_headers(int nfiles, char** files, int* ranks_out, int* rs_out, i
                m[any].red, wr, kind, gid + 1, groups, r + 1, ranks);
     }
   }
-  *ranks_out = ranks;
   *rs_out = rs;
   *enc_out = enc;
-  *m_out = m;
-  *group_out = group;
   return 0;
+}
+
+static void free_set(member* m, int ranks, htree* group) {
+  for (int r = 0; m && r < ranks; ++r) {
+    for (int k = 0; m[r].paths && k < m[r].nfiles; ++k) free(m[r].paths[k]);
+    free(m[r].paths);
+    free(m[r].sizes);
+    ht_free(m[r].hash);
+  }
+  free(m);
+  ht_free(group);
 }
 
 /* header of member r's redundancy file: its hash and its left neighbours'
@@ -263,8 +277,15 @@ int main(int argc, char** argv) {
   htree* group = NULL;
   int* missing = NULL;
   int nmissing = 0;
+  int status = 1;
+  int* nfiles = NULL;
+  int* writable = NULL;
+  const char** red = NULL;
+  unsigned long long* hdr = NULL;
+  const char** paths = NULL;
+  unsigned long long* sizes = NULL;
   if (hdr_mode) {
-    if (load_headers(argc - 2, argv + 2, &ranks, &rs_scheme, &encoding, &m, &group) != 0) return 1;
+    if (load_headers(argc - 2, argv + 2, &ranks, &rs_scheme, &encoding, &m, &group) != 0) goto out;
     missing = calloc((size_t) ranks, sizeof(int));
     for (int r = 0; r < ranks; ++r) {
       /* no readable header, parity cut short, or a data file absent / resized */
@@ -278,15 +299,17 @@ int main(int argc, char** argv) {
     encoding = rs_scheme ? atoi(argv[3]) : 1;
     if (ranks < 2 || encoding < 1 || encoding >= ranks) {
       fprintf(stderr, "redset_hip_rebuild: bad ranks/encoding\n");
-      return 2;
+      ranks = 0;
+      status = 2;
+      goto out;
     }
     m = calloc((size_t) ranks, sizeof(member));
     missing = calloc((size_t) ranks, sizeof(int));
     for (int r = 0; r < ranks; ++r) {
-      if (read_manifest(argv[4], r, &m[r]) != 0) return 1;
+      if (read_manifest(argv[4], r, &m[r]) != 0) goto out;
       if (m[r].chunk != m[0].chunk) {
         fprintf(stderr, "redset_hip_rebuild: members disagree on the chunk size\n");
-        return 1;
+        goto out;
       }
       /* expected redundancy file: header + encoding chunks */
       int gone = !file_ok(m[r].red, m[r].header + (unsigned long long) encoding * m[r].chunk);
@@ -298,11 +321,12 @@ int main(int argc, char** argv) {
   if (nmissing == 0) {
     printf("{\"scheme\": \"%s\", \"ranks\": %d, \"encoding\": %d, \"missing\": [], \"rebuilt_bytes\": 0}\n",
            scheme_name, ranks, encoding);
-    return 0;
+    status = 0;
+    goto out;
   }
   if (nmissing > encoding) {
     fprintf(stderr, "redset_hip_rebuild: %d members missing, the set tolerates %d\n", nmissing, encoding);
-    return 1;
+    goto out;
   }
 
   /* regenerate the headers of the missing members' redundancy files */
@@ -313,7 +337,7 @@ int main(int argc, char** argv) {
         int fd = open(x->paths[k], O_WRONLY | O_CREAT | O_TRUNC, 0600);
         if (fd < 0 || close(fd) != 0) {
           fprintf(stderr, "redset_hip_rebuild: create %s: %s\n", x->paths[k], strerror(errno));
-          return 1;
+          goto out;
         }
       }
       htree* h = member_header(m, ranks, missing[i], rs_scheme ? encoding : 1, group);
@@ -322,7 +346,7 @@ int main(int argc, char** argv) {
       ht_free(h);
       if (hs < 0 || close(fd) != 0) {
         fprintf(stderr, "redset_hip_rebuild: write header %s: %s\n", x->red, strerror(errno));
-        return 1;
+        goto out;
       }
       x->header = (unsigned long long) hs;
       continue;
@@ -337,23 +361,25 @@ int main(int argc, char** argv) {
       fclose(hf);
     }
     int fd = open(x->red, O_WRONLY | O_CREAT | O_TRUNC, 0600);
-    if (fd < 0 || write(fd, h, x->header) != (ssize_t) x->header || close(fd) != 0) {
-      fprintf(stderr, "redset_hip_rebuild: write header %s: %s\n", x->red, strerror(errno));
-      return 1;
-    }
+    int bad = fd < 0 || write(fd, h, x->header) != (ssize_t) x->header;
+    if (fd >= 0 && close(fd) != 0) bad = 1;
     free(h);
+    if (bad) {
+      fprintf(stderr, "redset_hip_rebuild: write header %s: %s\n", x->red, strerror(errno));
+      goto out;
+    }
   }
 
   /* one fileio over the whole set; the missing members' data files are
    * (re)created at their recorded sizes */
-  int* nfiles = calloc((size_t) ranks, sizeof(int));
-  int* writable = calloc((size_t) ranks, sizeof(int));
-  const char** red = calloc((size_t) ranks, sizeof(char*));
-  unsigned long long* hdr = calloc((size_t) ranks, sizeof(unsigned long long));
+  nfiles = calloc((size_t) ranks, sizeof(int));
+  writable = calloc((size_t) ranks, sizeof(int));
+  red = calloc((size_t) ranks, sizeof(char*));
+  hdr = calloc((size_t) ranks, sizeof(unsigned long long));
   int total = 0;
   for (int r = 0; r < ranks; ++r) total += m[r].nfiles;
-  const char** paths = calloc((size_t) total + 1, sizeof(char*));
-  unsigned long long* sizes = calloc((size_t) total + 1, sizeof(unsigned long long));
+  paths = calloc((size_t) total + 1, sizeof(char*));
+  sizes = calloc((size_t) total + 1, sizeof(unsigned long long));
   for (int r = 0, k = 0; r < ranks; ++r) {
     nfiles[r] = m[r].nfiles;
     red[r] = m[r].red;
@@ -369,7 +395,7 @@ int main(int argc, char** argv) {
   redset_hip_fileio* fio = NULL;
   if (redset_hip_fileio_create(ranks, nfiles, paths, sizes, red, hdr, (size_t) m[0].chunk, writable, &io, &fio) != 0) {
     fprintf(stderr, "redset_hip_rebuild: %s\n", redset_hip_last_error());
-    return 1;
+    goto out;
   }
   redset_hip_stream_stats st;
   memset(&st, 0, sizeof(st));
@@ -403,5 +429,15 @@ int main(int argc, char** argv) {
   printf("], \"ok\": %s, \"metadata_ok\": %s, \"seconds\": %.6f, \"bytes_read\": %llu, \"bytes_written\": %llu, \"GBps\": %.3f}\n",
          rc == 0 ? "true" : "false", meta_ok ? "true" : "false", st.seconds, st.bytes_read, st.bytes_written,
          st.seconds > 0 ? (double) (st.bytes_read + st.bytes_written) / st.seconds / 1e9 : 0.0);
-  return rc == 0 ? 0 : 1;
+  status = rc == 0 ? 0 : 1;
+out:
+  free(nfiles);
+  free(writable);
+  free(red);
+  free(hdr);
+  free(paths);
+  free(sizes);
+  free(missing);
+  free_set(m, ranks, group);
+  return status;
 }

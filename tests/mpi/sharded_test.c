@@ -213,6 +213,19 @@ int main(int argc, char** argv) {
     (void) hipStreamDestroy(stream);
   }
   ro_rs_delete(ORACLE);
+  for (int m = 0; m < nm; ++m) {
+    free(want_l[m]);
+    free(want_p[m]);
+  }
+  free(want_l);
+  free(want_p);
+  free(HD);
+  free(HP);
+  free(GD);
+  free(GP);
+  free(host);
+  free(slot);
+  free(count);
   MPI_Finalize();
   return all ? 0 : 1;
 }

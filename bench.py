@@ -385,6 +385,11 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
                       device="cuda" if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     value = world * runner.algorithmic_bytes("rebuild") / s_step / 1e9
+    # untimed diagnostic: the same rebuild with its three phases one after
+    # another (no overlap across sets), timed apart by events on rank 0
+    pipelined_event_ms = runner.phase_ms().get("rebuild_start->done")
+    runner.phased = True
+    timed(lambda i: runner.rebuild(), 3, 1, True, before=runner.reset_timing)
     out = {
         "workload": (f"{world} sets of p={p} (RS({p - e}+{e}), chunk {chunk >> 20} MiB), members round-robin over "
                      f"{world} GPUs; rebuild of members {lost} of every set, column-sharded (BASELINE.json configs[3])"),
@@ -393,6 +398,8 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
         "frac": round(value / world / HBM_PEAK_GBPS, 4),
         "ms_per_step": round(s_step * 1e3, 4),
         "bit_exact": bool(ok.item()),
+        "schedule": "sets pipelined: set k+1's gather overlaps set k's gf_mac (redset_hip_sharded_execute)",
+        "pipelined_event_ms_rank0": pipelined_event_ms,
     }
     out.update(runner.report(s_step, "rebuild"))
     return out

@@ -318,7 +318,12 @@ size_t redset_hip_shard_slice_bytes(size_t chunk_size, int world);
 int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
                                const redset_hip_shard_layout* layout, const redset_hip_transport* transport,
                                const redset_hip_compute* compute, redset_hip_sharded** out);
-/* All three phases (gather, compute, return) on `stream`. */
+/* All three phases, ordered after the work already on `stream`; work
+ * enqueued on `stream` afterwards sees the results. With the HIP plans as
+ * compute (compute == NULL at plan time) the sets are pipelined: every set's
+ * gather and return is an exchange of its own on a second stream the plan
+ * owns, so set k+1's gather (and the first returns) overlap set k's gf_mac on
+ * `stream`. With a compute callback the phases run one after another. */
 int redset_hip_sharded_execute(redset_hip_sharded* plan, void* stream);
 /* One phase (REDSET_HIP_PHASE_*), so callers can time them apart. */
 int redset_hip_sharded_execute_phase(redset_hip_sharded* plan, int phase, void* stream);

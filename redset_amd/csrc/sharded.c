@@ -14,6 +14,7 @@
  * r whole (:606-611); here every GPU solves its column slice of every stripe,
  * so the work splits evenly whatever p and the number of GPUs.
  */
+#include <hip/hip_runtime_api.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -147,7 +148,15 @@ struct redset_hip_sharded {
   int p, e, missing;
   int lost[MAX_RANKS];
   size_t W;
+  /* the exchanges, set by set: set k's transfers are gather.v[goff[k] ..
+   * goff[k+1]) and ret.v[roff[k] .. roff[k+1]); a phase runs all of them */
   xlist gather, ret;
+  int* goff;                       /* [nsets + 1] */
+  int* roff;                       /* [nsets + 1] */
+  /* pipelined execute (HIP compute): a stream for the exchanges, two events */
+  hipStream_t xstream;
+  hipEvent_t ev_x;                 /* exchange stream -> caller's stream */
+  hipEvent_t* ev_c;                /* [nsets] set k's compute done */
   /* compute per set: HIP plans, or the member pointers for the callback */
   redset_hip_plan** plans;         /* [nsets] (NULL entries when my slice is empty) */
   unsigned char** lofi;            /* [nsets * p] */
@@ -190,6 +199,95 @@ static int plan_inputs(const redset_hip_rs* rs, int p, int e, int kind, int miss
 static int cell_of(int p, int e, int r, int c) {
   const int enc = redset_hip_rs_get_encoding_id(p, e, r, c);
   return enc < p ? redset_hip_rs_get_data_id(p, e, r, c) : -(1 + (enc - p));
+}
+
+/* planning context: the layout and what this process is */
+typedef struct {
+  const redset_hip_shard_layout* L;
+  const int* by_slot;         /* (h, j) -> member, or -1 */
+  const unsigned char* need;  /* [p * p] member r's cell in stripe c is read */
+  int p, e, d, mh, world, me, kind, missing;
+  const int* lost;
+  size_t W;
+} pctx;
+
+/* addresses in this process's buffers (include/redset_hip.h layout) */
+static unsigned char* hd(const pctx* C, int q, int j, int s) {
+  return C->L->hosted_data + (((size_t) q * C->mh + j) * C->d + s) * C->W;
+}
+static unsigned char* hp(const pctx* C, int q, int j, int i) {
+  return C->L->hosted_parity + (((size_t) q * C->mh + j) * C->e + i) * C->W;
+}
+static unsigned char* gd(const pctx* C, int h, int j, int s) {
+  return C->L->gathered_data + (((size_t) h * C->mh + j) * C->d + s) * C->W;
+}
+static unsigned char* gp(const pctx* C, int h, int j, int i) {
+  return C->L->gathered_parity + (((size_t) h * C->mh + j) * C->e + i) * C->W;
+}
+
+/* does some stripe read member r's data cell x (pass 0) / parity slot x (pass 1)? */
+static int wanted(const pctx* C, int r, int pass, int x) {
+  for (int c = 0; c < C->p; ++c)
+    if (C->need[r * C->p + c] && cell_of(C->p, C->e, r, c) == (pass == 0 ? x : -(1 + x))) return 1;
+  return 0;
+}
+
+/* set k's gather: slice g of every needed cell of every surviving member of
+ * the set goes from its host to process g; data rows then parity rows,
+ * members in slot order (both ends of a pair walk the same rows) */
+static int plan_gather(const pctx* C, int k, exch* G) {
+  const int me = C->me;
+  int rc = 0;
+  for (int g = 0; g < C->world && !rc; ++g) {
+    for (int pass = 0; pass < 2 && !rc; ++pass) {
+      const int ncell = pass == 0 ? C->d : C->e;
+      for (int j = 0; j < C->mh && !rc; ++j) { /* what I send to g (g == me: copy) */
+        const int m = C->by_slot[(size_t) me * C->mh + j];
+        if (m < 0 || m / C->p != k) continue;
+        for (int x = 0; x < ncell && !rc; ++x) {
+          if (!wanted(C, m % C->p, pass, x)) continue;
+          unsigned char* src = pass == 0 ? hd(C, g, j, x) : hp(C, g, j, x);
+          if (g == me) rc = ex_copy(G, pass == 0 ? gd(C, me, j, x) : gp(C, me, j, x), src, C->W);
+          else rc = ex_send(G, g, src, C->W);
+        }
+      }
+      if (g == me) continue;
+      for (int j = 0; j < C->mh && !rc; ++j) { /* my slice of g's members' needed cells */
+        const int m = C->by_slot[(size_t) g * C->mh + j];
+        if (m < 0 || m / C->p != k) continue;
+        for (int x = 0; x < ncell && !rc; ++x)
+          if (wanted(C, m % C->p, pass, x)) rc = ex_recv(G, g, pass == 0 ? gd(C, g, j, x) : gp(C, g, j, x), C->W);
+      }
+    }
+  }
+  return rc;
+}
+
+/* set k's return: the outputs (encode: every member's parity; rebuild: every
+ * cell of the lost members) go from each process's gathered slots to the
+ * member's host: data rows, then parity rows, members in set order */
+static int plan_return(const pctx* C, int k, exch* R) {
+  int rc = 0;
+  for (int pass = 0; pass < 2 && !rc; ++pass) {
+    if (pass == 0 && C->kind == REDSET_HIP_PLAN_RS_ENCODE) continue; /* encode returns parity only */
+    for (int m = k * C->p; m < (k + 1) * C->p && !rc; ++m) {
+      int is_out = C->kind == REDSET_HIP_PLAN_RS_ENCODE;
+      for (int i = 0; i < C->missing; ++i) is_out |= C->lost[i] == m % C->p;
+      if (!is_out) continue;
+      const int h = C->L->host[m], j = C->L->slot[m];
+      const size_t len = (size_t) (pass == 0 ? C->d : C->e) * C->W;
+      unsigned char* mine = pass == 0 ? gd(C, h, j, 0) : gp(C, h, j, 0);
+      if (h != C->me) {
+        rc = ex_send(R, h, mine, len);
+        continue;
+      }
+      for (int g = 0; g < C->world && !rc; ++g) {
+        unsigned char* dst = pass == 0 ? hd(C, g, j, 0) : hp(C, g, j, 0);
+        rc = g == C->me ? ex_copy(R, dst, mine, len) : ex_recv(R, g, dst, len);
+      }
+    }
+  }
+  return rc;
 }
 
 int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
@@ -264,75 +362,28 @@ int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, c
   for (int m = 0; m < nm; ++m) by_slot[(size_t) L->host[m] * mh + L->slot[m]] = m;
   if ((rc = plan_inputs(rs, p, e, kind, missing, rebuild_ranks, need))) goto done;
 
-  /* addresses in this process's buffers */
-#define HD(q, j, s) (L->hosted_data + ((((size_t) (q) * mh + (j)) * d + (s)) * W))
-#define HP(q, j, i) (L->hosted_parity + ((((size_t) (q) * mh + (j)) * e + (i)) * W))
-#define GD(h, j, s) (L->gathered_data + ((((size_t) (h) * mh + (j)) * d + (s)) * W))
-#define GP(h, j, i) (L->gathered_parity + ((((size_t) (h) * mh + (j)) * e + (i)) * W))
-
-  /* gather: slice g of every needed cell of every surviving member goes from
-   * its host to process g; data rows then parity rows, members in slot order */
-  for (int g = 0; g < world && !rc; ++g) {
-    for (int pass = 0; pass < 2 && !rc; ++pass) {
-      const int ncell = pass == 0 ? d : e;
-      /* what I send to g (g == me: copy) */
-      for (int j = 0; j < mh && !rc; ++j) {
-        const int m = by_slot[(size_t) me * mh + j];
-        if (m < 0) continue;
-        const int r = m % p;
-        for (int x = 0; x < ncell && !rc; ++x) {
-          int wanted = 0;
-          for (int c = 0; c < p && !wanted; ++c)
-            if (need[r * p + c] && cell_of(p, e, r, c) == (pass == 0 ? x : -(1 + x))) wanted = 1;
-          if (!wanted) continue;
-          unsigned char* src = pass == 0 ? HD(g, j, x) : HP(g, j, x);
-          if (g == me) rc = ex_copy(&G, pass == 0 ? GD(me, j, x) : GP(me, j, x), src, W);
-          else rc = ex_send(&G, g, src, W);
-        }
-      }
-      if (g == me) continue;
-      /* what I receive from g: my slice of g's members' needed cells */
-      for (int j = 0; j < mh && !rc; ++j) {
-        const int m = by_slot[(size_t) g * mh + j];
-        if (m < 0) continue;
-        const int r = m % p;
-        for (int x = 0; x < ncell && !rc; ++x) {
-          int wanted = 0;
-          for (int c = 0; c < p && !wanted; ++c)
-            if (need[r * p + c] && cell_of(p, e, r, c) == (pass == 0 ? x : -(1 + x))) wanted = 1;
-          if (wanted) rc = ex_recv(&G, g, pass == 0 ? GD(g, j, x) : GP(g, j, x), W);
-        }
-      }
-    }
+  pctx C = {L, by_slot, need, p, e, d, mh, world, me, kind, missing, P->lost, W};
+  P->goff = calloc((size_t) L->nsets + 1, sizeof(int));
+  P->roff = calloc((size_t) L->nsets + 1, sizeof(int));
+  if (!P->goff || !P->roff) {
+    rc = sfail("out of host memory");
+    goto done;
   }
-
-  /* return: the outputs (encode: every member's parity; rebuild: every cell
-   * of the lost members) go from each process's gathered slots to the
-   * member's host: data rows, then parity rows, members in set order */
-  for (int pass = 0; pass < 2 && !rc; ++pass) {
-    if (pass == 0 && kind == REDSET_HIP_PLAN_RS_ENCODE) continue; /* encode returns parity only */
-    for (int m = 0; m < nm && !rc; ++m) {
-      const int r = m % p;
-      int is_out = kind == REDSET_HIP_PLAN_RS_ENCODE;
-      for (int i = 0; i < missing; ++i) is_out |= P->lost[i] == r;
-      if (!is_out) continue;
-      const int h = L->host[m], j = L->slot[m];
-      const size_t len = (size_t) (pass == 0 ? d : e) * W;
-      unsigned char* mine = pass == 0 ? GD(h, j, 0) : GP(h, j, 0);
-      if (h != me) {
-        rc = ex_send(&R, h, mine, len);
-        continue;
-      }
-      for (int g = 0; g < world && !rc; ++g) {
-        unsigned char* dst = pass == 0 ? HD(g, j, 0) : HP(g, j, 0);
-        rc = g == me ? ex_copy(&R, dst, mine, len) : ex_recv(&R, g, dst, len);
-      }
-    }
+  /* set by set, so a set's exchanges can run on their own (pipelined execute) */
+  for (int k = 0; k < L->nsets && !rc; ++k) {
+    rc = plan_gather(&C, k, &G);
+    if (!rc) rc = ex_flatten(&G, &P->gather, &P->info.gather_messages, &P->info.gather_bytes_sent,
+                             &P->info.gather_bytes_recv, &P->info.local_bytes);
+    if (!rc) rc = plan_return(&C, k, &R);
+    if (!rc) rc = ex_flatten(&R, &P->ret, &P->info.return_messages, &P->info.return_bytes_sent,
+                             &P->info.return_bytes_recv, &P->info.local_bytes);
+    P->goff[k + 1] = P->gather.n;
+    P->roff[k + 1] = P->ret.n;
+    ex_free(&G);
+    ex_free(&R);
+    if (!rc) rc = ex_init(&G, world, me);
+    if (!rc) rc = ex_init(&R, world, me);
   }
-  if (!rc) rc = ex_flatten(&G, &P->gather, &P->info.gather_messages, &P->info.gather_bytes_sent,
-                           &P->info.gather_bytes_recv, &P->info.local_bytes);
-  if (!rc) rc = ex_flatten(&R, &P->ret, &P->info.return_messages, &P->info.return_bytes_sent,
-                           &P->info.return_bytes_recv, &P->info.local_bytes);
   if (rc) goto done;
 
   /* compute: every set over my slices in the gathered layout (cell stride W) */
@@ -344,8 +395,8 @@ int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, c
     goto done;
   }
   for (int m = 0; m < nm; ++m) {
-    P->lofi[m] = GD(L->host[m], L->slot[m], 0);
-    P->parity[m] = GP(L->host[m], L->slot[m], 0);
+    P->lofi[m] = gd(&C, L->host[m], L->slot[m], 0);
+    P->parity[m] = gp(&C, L->host[m], L->slot[m], 0);
   }
   const size_t n = P->info.my_slice_len;
   P->info.compute_bytes = (unsigned long long) L->nsets * p * (d + (kind == REDSET_HIP_PLAN_RS_ENCODE ? e : missing)) * n;
@@ -355,11 +406,6 @@ int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, c
     rc = kind == REDSET_HIP_PLAN_RS_ENCODE ? redset_hip_rs_plan_encode(rs, lf, pr, n, W, &P->plans[k])
                                            : redset_hip_rs_plan_rebuild(rs, missing, P->lost, lf, pr, n, W, &P->plans[k]);
   }
-#undef HD
-#undef HP
-#undef GD
-#undef GP
-
 done:
   ex_free(&G);
   ex_free(&R);
@@ -373,40 +419,92 @@ done:
   return REDSET_SUCCESS;
 }
 
+static int compute_set(redset_hip_sharded* P, int k, void* stream) {
+  const size_t n = P->info.my_slice_len;
+  if (n == 0) return REDSET_SUCCESS;
+  if (P->comp.run) {
+    if (P->comp.run(P->comp.ctx, P->info.kind, P->missing, P->lost, P->lofi + (size_t) k * P->p,
+                    P->parity + (size_t) k * P->p, n, P->W, stream) != 0)
+      return sfail("sharded compute callback failed (set %d)", k);
+    return REDSET_SUCCESS;
+  }
+  return redset_hip_plan_execute(P->plans[k], stream);
+}
+
+/* transfers [lo, hi) of list L as one exchange */
+static int exchange(redset_hip_sharded* P, const xlist* L, int lo, int hi, void* stream, const char* what) {
+  if (hi > lo && P->tr.exchange(P->tr.ctx, L->v + lo, hi - lo, stream) != 0)
+    return sfail("sharded %s: transport exchange failed", what);
+  return REDSET_SUCCESS;
+}
+
 int redset_hip_sharded_execute_phase(redset_hip_sharded* P, int phase, void* stream) {
   if (!P) return sfail("null sharded plan");
   switch (phase) {
     case REDSET_HIP_PHASE_GATHER:
-      if (P->gather.n && P->tr.exchange(P->tr.ctx, P->gather.v, P->gather.n, stream) != 0)
-        return sfail("sharded gather: transport exchange failed");
+      return exchange(P, &P->gather, 0, P->gather.n, stream, "gather");
+    case REDSET_HIP_PHASE_COMPUTE:
+      for (int k = 0; k < P->info.nsets; ++k)
+        if (compute_set(P, k, stream)) return REDSET_FAILURE;
       return REDSET_SUCCESS;
-    case REDSET_HIP_PHASE_COMPUTE: {
-      const size_t n = P->info.my_slice_len;
-      if (n == 0) return REDSET_SUCCESS;
-      for (int k = 0; k < P->info.nsets; ++k) {
-        if (P->comp.run) {
-          if (P->comp.run(P->comp.ctx, P->info.kind, P->missing, P->lost, P->lofi + (size_t) k * P->p,
-                          P->parity + (size_t) k * P->p, n, P->W, stream) != 0)
-            return sfail("sharded compute callback failed (set %d)", k);
-        } else if (redset_hip_plan_execute(P->plans[k], stream)) {
-          return REDSET_FAILURE;
-        }
-      }
-      return REDSET_SUCCESS;
-    }
     case REDSET_HIP_PHASE_RETURN:
-      if (P->ret.n && P->tr.exchange(P->tr.ctx, P->ret.v, P->ret.n, stream) != 0)
-        return sfail("sharded return: transport exchange failed");
-      return REDSET_SUCCESS;
+      return exchange(P, &P->ret, 0, P->ret.n, stream, "return");
     default:
       return sfail("unknown sharded phase %d", phase);
   }
 }
 
-int redset_hip_sharded_execute(redset_hip_sharded* P, void* stream) {
-  for (int ph = REDSET_HIP_PHASE_GATHER; ph <= REDSET_HIP_PHASE_RETURN; ++ph)
-    if (redset_hip_sharded_execute_phase(P, ph, stream)) return REDSET_FAILURE;
+static int hfail(const char* what, hipError_t e) { return sfail("sharded execute: %s: %s", what, hipGetErrorString(e)); }
+
+/* Sets pipelined over two streams: set k+1's gather runs on the plan's
+ * exchange stream while set k's gf_mac runs on the caller's, and the returns
+ * follow the gathers there, each after its own set's compute (so the last
+ * compute overlaps the first returns). Exchange stream: G0 .. G(n-1) R0 ..
+ * R(n-1); caller's stream: C0 .. C(n-1), each after its gather. Both start
+ * after the work already on `stream`, and `stream` resumes after the last
+ * return. A transport that completes its exchange before returning (MPI)
+ * overlaps the same way: the host runs gather k+1 while the GPU computes k. */
+static int execute_pipelined(redset_hip_sharded* P, hipStream_t s) {
+  hipError_t e;
+  const int n = P->info.nsets;
+  if (!P->xstream) {
+    P->ev_c = calloc((size_t) n, sizeof(hipEvent_t));
+    if (!P->ev_c) return sfail("out of host memory");
+    if ((e = hipStreamCreateWithFlags(&P->xstream, hipStreamNonBlocking)) != hipSuccess) return hfail("stream", e);
+    if ((e = hipEventCreateWithFlags(&P->ev_x, hipEventDisableTiming)) != hipSuccess) return hfail("event", e);
+    for (int k = 0; k < n; ++k)
+      if ((e = hipEventCreateWithFlags(&P->ev_c[k], hipEventDisableTiming)) != hipSuccess) return hfail("event", e);
+  }
+  hipStream_t x = P->xstream;
+  /* the exchange stream starts after the caller's work (ev_c[0] is free until
+   * compute 0 records it) */
+  if ((e = hipEventRecord(P->ev_c[0], s)) != hipSuccess || (e = hipStreamWaitEvent(x, P->ev_c[0], 0)) != hipSuccess)
+    return hfail("order after the caller's stream", e);
+  for (int k = 0; k < n; ++k) {
+    if (exchange(P, &P->gather, P->goff[k], P->goff[k + 1], x, "gather")) return REDSET_FAILURE;
+    if ((e = hipEventRecord(P->ev_x, x)) != hipSuccess || (e = hipStreamWaitEvent(s, P->ev_x, 0)) != hipSuccess)
+      return hfail("gather -> compute", e);
+    if (compute_set(P, k, s)) return REDSET_FAILURE;
+    if ((e = hipEventRecord(P->ev_c[k], s)) != hipSuccess) return hfail("compute event", e);
+  }
+  for (int k = 0; k < n; ++k) {
+    if (P->roff[k + 1] == P->roff[k]) continue;
+    if ((e = hipStreamWaitEvent(x, P->ev_c[k], 0)) != hipSuccess) return hfail("compute -> return", e);
+    if (exchange(P, &P->ret, P->roff[k], P->roff[k + 1], x, "return")) return REDSET_FAILURE;
+  }
+  if ((e = hipEventRecord(P->ev_x, x)) != hipSuccess || (e = hipStreamWaitEvent(s, P->ev_x, 0)) != hipSuccess)
+    return hfail("order the caller's stream after the returns", e);
   return REDSET_SUCCESS;
+}
+
+int redset_hip_sharded_execute(redset_hip_sharded* P, void* stream) {
+  if (!P) return sfail("null sharded plan");
+  if (P->comp.run) {
+    for (int ph = REDSET_HIP_PHASE_GATHER; ph <= REDSET_HIP_PHASE_RETURN; ++ph)
+      if (redset_hip_sharded_execute_phase(P, ph, stream)) return REDSET_FAILURE;
+    return REDSET_SUCCESS;
+  }
+  return execute_pipelined(P, (hipStream_t) stream);
 }
 
 int redset_hip_sharded_get_info(const redset_hip_sharded* P, redset_hip_sharded_info* info) {
@@ -419,6 +517,14 @@ void redset_hip_sharded_destroy(redset_hip_sharded* P) {
   if (!P) return;
   for (int k = 0; P->plans && k < P->info.nsets; ++k) redset_hip_plan_destroy(P->plans[k]);
   free(P->plans);
+  if (P->xstream) (void) hipStreamSynchronize(P->xstream);
+  for (int k = 0; P->ev_c && k < P->info.nsets; ++k)
+    if (P->ev_c[k]) (void) hipEventDestroy(P->ev_c[k]);
+  free(P->ev_c);
+  if (P->ev_x) (void) hipEventDestroy(P->ev_x);
+  if (P->xstream) (void) hipStreamDestroy(P->xstream);
+  free(P->goff);
+  free(P->roff);
   free(P->lofi);
   free(P->parity);
   free(P->gather.v);

@@ -182,6 +182,7 @@ class ShardedSetRunner:
         self.my_len = self.slice_len(rank)
         self._place()
         self.timing = self.device.type == "cuda"
+        self.phased = False
         self._events = []
         d, W, mh = self.d, self.W, p  # every GPU hosts p members
         u8 = dict(dtype=torch.uint8, device=self.device)
@@ -266,10 +267,18 @@ class ShardedSetRunner:
             self._events.append((name, ev))
 
     def _run(self, op: str) -> None:
+        """One execute: pipelined over the sets (redset_hip_sharded_execute:
+        set k+1's gather overlaps set k's gf_mac), or, with ``self.phased``,
+        the three phases one after another with events between them so
+        phase_ms() can split the time."""
         L = _lib.load()
         h = self._plans[op]
         stream = torch.cuda.current_stream().cuda_stream if self.device.type == "cuda" else None
         self._mark(f"{op}_start")
+        if not self.phased:
+            _lib.check(L.redset_hip_sharded_execute(h, stream), f"sharded {op}")
+            self._mark(f"{op}_done")
+            return
         _lib.check(L.redset_hip_sharded_execute_phase(h, _lib.PHASE_GATHER, stream), f"sharded {op} gather")
         self._mark(f"{op}_gathered")
         _lib.check(L.redset_hip_sharded_execute_phase(h, _lib.PHASE_COMPUTE, stream), f"sharded {op} compute")

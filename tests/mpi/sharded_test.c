@@ -8,6 +8,9 @@
  * encode / rebuild without a GPU.
  *
  * usage: sharded_test [--gpu] <p> <e> <chunk> [lost ranks...]   (world = MPI size)
+ * SHARDED_TEST_REPS=<n> (--gpu): after the checks, time n rebuilds with the
+ * pipelined execute and n with the three phases one after another (slowest
+ * process, ms per rebuild).
  * --gpu: the slabs live in HBM, the compute is the HIP gf_mac plans and the
  * MPI transport stages through pinned host memory (every process may share
  * one GPU) -- the whole sharded path with the real kernels at world > 1.
@@ -194,6 +197,22 @@ int main(int argc, char** argv) {
     }
     if (rbad) fprintf(stderr, "rank %d: %d bytes differ after the rebuild\n", me, rbad);
     bad += rbad;
+    const char* reps_env = getenv("SHARDED_TEST_REPS");
+    const int reps = gpu && reps_env ? atoi(reps_env) : 0;
+    for (int mode = 0; ok && !rbad && reps > 0 && mode < 2; ++mode) {
+      /* repeated rebuilds rewrite the same bytes; mode 0 pipelined, 1 phased */
+      MPI_Barrier(MPI_COMM_WORLD);
+      double t0 = MPI_Wtime();
+      for (int i = 0; ok && i < reps; ++i) {
+        if (mode == 0) ok = redset_hip_sharded_execute(reb, stream) == 0;
+        for (int ph = REDSET_HIP_PHASE_GATHER; ok && mode == 1 && ph <= REDSET_HIP_PHASE_RETURN; ++ph)
+          ok = redset_hip_sharded_execute_phase(reb, ph, stream) == 0;
+      }
+      ok = ok && hipStreamSynchronize(stream) == hipSuccess;
+      double dt = (MPI_Wtime() - t0) * 1e3 / reps, dmax = 0;
+      MPI_Allreduce(&dt, &dmax, 1, MPI_DOUBLE, MPI_MAX, MPI_COMM_WORLD);
+      if (me == 0) printf("timing: %s rebuild %.3f ms\n", mode == 0 ? "pipelined" : "phased", dmax);
+    }
     redset_hip_sharded_info info;
     if (ok && redset_hip_sharded_get_info(reb, &info) == 0)
       printf("rank %d: rebuild gather %llu B sent in %d messages, return %llu B sent, local %llu B\n", me,

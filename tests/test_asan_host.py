@@ -18,6 +18,7 @@ import subprocess
 import numpy as np
 import pytest
 
+from proc import run_group
 from redset_amd import header as H
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -49,7 +50,7 @@ def _clean(res):
 def test_sharded_planner_asan(asan_build, np_, args):
     cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", os.path.join(asan_build, "sharded_test")] + \
         [str(a) for a in args]
-    res = subprocess.run(cmd, capture_output=True, text=True, timeout=180, env=ENV)
+    res = run_group(cmd, 180, env=ENV)
     assert _clean(res), res.stderr[-4000:]
     assert res.returncode == 0, res.stdout + res.stderr[-4000:]
 

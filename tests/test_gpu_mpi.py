@@ -11,10 +11,13 @@ import subprocess
 import numpy as np
 import pytest
 
+from proc import run_group
+
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-RANK_TEST = os.path.join(ROOT, "tests", "mpi", "build", "rank_test")
+# RANK_TEST_BIN: another build of the driver (tools/gpu_asan.sh: host ASan)
+RANK_TEST = os.environ.get("RANK_TEST_BIN") or os.path.join(ROOT, "tests", "mpi", "build", "rank_test")
 MPIRUN = "/opt/conda/bin/mpirun"
 
 
@@ -35,7 +38,7 @@ def _have():
 
 def _mpirun(np_, args, timeout=300):
     cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", RANK_TEST] + [str(a) for a in args]
-    return subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
+    return run_group(cmd, timeout)
 
 
 def _setup(tmp, p, d, rng, maxsize):
@@ -148,9 +151,10 @@ def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme
     else:
         args = [scheme, "encode", e, tmp, buf]
     cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST] + [str(a) for a in args]
-    res = subprocess.run(cmd, capture_output=True, text=True, timeout=90, env={**os.environ, **env})
+    res = run_group(cmd, 90, env={**os.environ, **env})
     assert res.returncode != 0, res.stdout + res.stderr  # every rank exits 1 (alltrue is false)
     assert "backend failed" in res.stderr
+    assert "Sanitizer" not in res.stderr, res.stderr[-4000:]  # tools/gpu_asan.sh builds
 
 
 @pytest.mark.parametrize("np_,p,e,chunk,lost", [(2, 11, 3, 300_001, [1, 2]), (4, 20, 4, 65536, [0, 5, 19]),
@@ -161,12 +165,12 @@ def test_mpi_sharded_gpu(np_, p, e, chunk, lost):
     through pinned memory (the processes share the box's one GPU; RCCL needs
     one GPU per rank). tests/mpi/sharded_test.c --gpu checks hosted parity and
     the rebuilt members against the oracle."""
-    driver = os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
+    driver = os.environ.get("SHARDED_TEST_BIN") or os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
     if not _have() or not os.path.exists(driver):
         pytest.skip("needs a GPU, MPICH and tests/mpi/build/sharded_test")
     cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", driver, "--gpu", str(p), str(e), str(chunk)] + \
         [str(x) for x in lost]
-    res = subprocess.run(cmd, capture_output=True, text=True, timeout=120)
+    res = run_group(cmd, 120)
     assert res.returncode == 0, res.stdout + res.stderr
     assert res.stdout.count("rebuild gather") == np_
 

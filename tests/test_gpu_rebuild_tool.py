@@ -15,7 +15,9 @@ import pytest
 pytestmark = pytest.mark.gpu
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-TOOL = os.path.join(ROOT, "redset_amd", "bin", "redset_hip_rebuild")
+# REDSET_HIP_REBUILD_TOOL: another build of the tool (tools/gpu_asan.sh runs
+# the host-ASan one from tests/asan)
+TOOL = os.environ.get("REDSET_HIP_REBUILD_TOOL") or os.path.join(ROOT, "redset_amd", "bin", "redset_hip_rebuild")
 
 
 def _need():
@@ -108,3 +110,4 @@ def test_offline_rebuild_too_many_missing(oracle, tmp_path):
         os.unlink(reds[r])
     res = subprocess.run([TOOL, "rs", "5", "2", tmp], capture_output=True, text=True, timeout=300)
     assert res.returncode != 0 and "tolerates" in res.stderr
+    assert "Sanitizer" not in res.stderr, res.stderr[-4000:]  # tools/gpu_asan.sh builds

@@ -10,6 +10,8 @@ import subprocess
 
 import pytest
 
+from proc import run_group
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DRIVER = os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
 MPIRUN = "/opt/conda/bin/mpirun"
@@ -36,6 +38,6 @@ def test_sharded_plan_over_mpi_matches_oracle(oracle, np_, p, e, chunk, lost):
     if not _have():
         pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
     cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", DRIVER, str(p), str(e), str(chunk)] + [str(x) for x in lost]
-    res = subprocess.run(cmd, capture_output=True, text=True, timeout=120, cwd="/tmp")
+    res = run_group(cmd, 120, cwd="/tmp")
     assert res.returncode == 0, res.stdout + res.stderr
     assert res.stdout.count("rebuild gather") == np_

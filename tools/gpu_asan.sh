@@ -1,0 +1,23 @@
+#!/bin/bash
+# Host-code AddressSanitizer on the GPU box: the offline rebuild tool (the
+# streaming pipeline + file I/O), the per-rank MPI backends and the sharded
+# driver, built by tests/asan/Makefile with -Xarch_host ASan only (no GPU
+# instrumentation), driven by their own GPU tests.
+# Leak checking is off by default here (DETECT_LEAKS=1 turns it on): at exit
+# LeakSanitizer's stop-the-world intermittently hung processes that had the
+# HIP runtime's threads running (twice in two runs, a different test each
+# time; never without it). The CPU-only runs (tests/test_asan_host.py) keep it.
+# usage: tools/gpu_asan.sh <tag>
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+OUT=gpurun_out/${1:-asan}; mkdir -p "$OUT"
+B=tests/asan/build
+export ASAN_OPTIONS="verify_asan_link_order=0:detect_leaks=${DETECT_LEAKS:-0}:exitcode=86"
+export LSAN_OPTIONS="suppressions=$PWD/tests/asan/lsan.supp"
+export REDSET_HIP_REBUILD_TOOL=$PWD/$B/redset_hip_rebuild RANK_TEST_BIN=$PWD/$B/rank_test SHARDED_TEST_BIN=$PWD/$B/sharded_test
+timeout -k 10 600 python -u -m pytest -x -v --timeout 100 --timeout-method thread \
+  tests/test_gpu_rebuild_tool.py tests/test_gpu_mpi.py > "$OUT/asan_tests.log" 2>&1
+s=$?
+tail -5 "$OUT/asan_tests.log"
+grep -c "AddressSanitizer\|LeakSanitizer" "$OUT/asan_tests.log" || true
+exit $s

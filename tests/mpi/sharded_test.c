@@ -15,7 +15,8 @@
  * MPI transport stages through pinned host memory (every process may share
  * one GPU) -- the whole sharded path with the real kernels at world > 1.
  * Placement: `world` sets of p members, member m on process (m * 7 + 3) %
- * world, hosted slots in ascending member order. Exit 0 iff every process
+ * world (SHARDED_TEST_SEED=<s>: on a pseudo-random process), hosted slots in
+ * ascending member order. Exit 0 iff every process
  * found its hosted parity (after encode) and its lost members' cells (after
  * rebuild) equal to the oracle's.
  */
@@ -91,8 +92,10 @@ int main(int argc, char** argv) {
   int* slot = malloc(sizeof(int) * nm);
   int* count = calloc(world, sizeof(int));
   int mh = 0;
+  const char* seed_env = getenv("SHARDED_TEST_SEED");
   for (int m = 0; m < nm; ++m) {
-    host[m] = (m * 7 + 3) % world;
+    /* SHARDED_TEST_SEED: members on random processes (unbalanced allowed) */
+    host[m] = seed_env ? (int) (byte_of(0x7FFF, atoi(seed_env), (size_t) m) % world) : (m * 7 + 3) % world;
     slot[m] = count[host[m]]++;
     if (count[host[m]] > mh) mh = count[host[m]];
   }

@@ -208,3 +208,25 @@ def test_mpi_config0_xor_4_ranks_16MiB(oracle, tmp_path):
     assert os.path.getsize(files[2][0][0]) == size
     assert oracle.crc32(np.fromfile(files[2][0][0], dtype=np.uint8)) == crc
     assert np.array_equal(np.fromfile(reds[2], dtype=np.uint8)[4096:], want[2])
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_mpi_sharded_gpu_random(seed):
+    """tests/test_mpi_sharded.py's random shapes and placements with the HIP
+    kernels and the pipelined execute (slabs in HBM, MPI transport staging
+    through pinned memory; the processes share the box's GPU)."""
+    driver = os.environ.get("SHARDED_TEST_BIN") or os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
+    if not _have() or not os.path.exists(driver):
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/sharded_test")
+    rng = np.random.default_rng(5000 + seed)
+    np_ = int(rng.integers(1, 5))
+    p = int(rng.integers(2, 24))
+    e = int(rng.integers(1, min(p - 1, 6) + 1))
+    chunk = int(rng.choice([1, 255, 257, int(rng.integers(2, 200_000))]))
+    m = int(rng.integers(1, e + 1))
+    lost = sorted(rng.choice(p, size=m, replace=False).tolist())
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", driver, "--gpu", str(p), str(e), str(chunk)] + \
+        [str(x) for x in lost]
+    res = run_group(cmd, 120, env={**os.environ, "SHARDED_TEST_SEED": str(seed)})
+    assert res.returncode == 0, (np_, p, e, chunk, lost, res.stdout + res.stderr)
+    assert res.stdout.count("rebuild gather") == np_

@@ -41,3 +41,25 @@ def test_sharded_plan_over_mpi_matches_oracle(oracle, np_, p, e, chunk, lost):
     res = run_group(cmd, 120, cwd="/tmp")
     assert res.returncode == 0, res.stdout + res.stderr
     assert res.stdout.count("rebuild gather") == np_
+
+
+@pytest.mark.parametrize("seed", range(30))
+def test_sharded_plan_random_shapes_and_placements(oracle, seed):
+    """Seeded random set shapes, erasures, chunk sizes, world sizes and
+    member placements (pseudo-random processes, unbalanced slot counts):
+    the planner's gather/return against the oracle's whole-set answer."""
+    if not _have():
+        pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
+    import numpy as np
+
+    rng = np.random.default_rng(4000 + seed)
+    np_ = int(rng.integers(1, 5))
+    p = int(rng.integers(2, 24))
+    e = int(rng.integers(1, min(p - 1, 6) + 1))
+    chunk = int(rng.choice([1, 255, 256, 257, int(rng.integers(2, 5000))]))
+    m = int(rng.integers(1, e + 1))
+    lost = sorted(rng.choice(p, size=m, replace=False).tolist())
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", DRIVER, str(p), str(e), str(chunk)] + [str(x) for x in lost]
+    res = run_group(cmd, 120, env={**os.environ, "SHARDED_TEST_SEED": str(seed)}, cwd="/tmp")
+    assert res.returncode == 0, (np_, p, e, chunk, lost, res.stdout + res.stderr)
+    assert res.stdout.count("rebuild gather") == np_

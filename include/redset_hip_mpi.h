@@ -50,6 +50,13 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
 int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
                                int fd_chunk, size_t chunk_size, size_t buf_size);
 
+/* The backends above keep a successful call's pinned host buffers, device
+ * buffers and stream for the next call (at most 256 MiB pinned, 1 GiB of
+ * device memory); REDSET_HIP_SCRATCH_CACHE=0 allocates and frees per call
+ * instead, as the reference does (src/redset_reedsolomon.c:298-302, :397-399).
+ * This frees the cache, e.g. from redset_finalize. */
+void redset_hip_rank_scratch_release(void);
+
 /* Transport of the sharded path (redset_hip_rs_sharded_plan) over MPI
  * point-to-point: MPI_Isend / MPI_Irecv of every message of an exchange,
  * then MPI_Waitall -- the reference's own primitives (src/redset_reedsolomon.c:

@@ -61,6 +61,7 @@ static redset_hip_rs* codec_for(int ranks, int encoding) {
 void redset_hip_backend_finalize(void) {
   redset_hip_rs_destroy(cached_rs);
   cached_rs = NULL;
+  redset_hip_rank_scratch_release();
 }
 
 int redset_reedsolomon_encode_hip(const redset_base* d, redset_lofi rsf, const char* chunk_file, int fd_xor,

@@ -34,8 +34,8 @@ int redset_xor_encode_hip(const redset_base* d, redset_lofi rsf, const char* chu
 int redset_xor_decode_hip(const redset_base* d, int root, redset_lofi rsf, const char* chunk_file, int fd_chunk,
                           size_t chunk_size);
 
-/* release the codec state the RS functions cache per (ranks, encoding);
- * call from redset_finalize (src/redset.c) */
+/* release the codec state the RS functions cache per (ranks, encoding) and
+ * the backends' scratch cache; call from redset_finalize (src/redset.c) */
 void redset_hip_backend_finalize(void);
 
 #ifdef __cplusplus

@@ -16,6 +16,7 @@
 
 #include <errno.h>
 #include <limits.h>
+#include <pthread.h>
 #include <hip/hip_runtime_api.h>
 #include <stdarg.h>
 #include <stdint.h>
@@ -40,51 +41,133 @@ static int fail(const char* fmt, ...) {
 
 static size_t min_sz(size_t a, size_t b) { return a < b ? a : b; }
 
-/* ---- page-locked host + device scratch and one stream, per call -------- */
+/* ---- page-locked host + device scratch and one stream ------------------- */
+/*
+ * The reference allocates its slice buffers per call (src/redset_reedsolomon.c:
+ * 298-302). Here a call's pinned host buffers, device buffers and stream go
+ * back to a small process-wide cache when the call succeeds and the next call
+ * takes them from there: pinning costs ~0.15 ms per MiB to allocate and free
+ * and a stream ~2.7 ms to create and destroy (profiles/r02_alloc_probe.jsonl),
+ * which is a large share of a small set's call. REDSET_HIP_SCRATCH_CACHE=0
+ * restores allocate-and-free per call; redset_hip_rank_scratch_release()
+ * frees the cache (e.g. at redset_finalize). A failed call frees its scratch.
+ */
+#define POOL_MAX 32
+#define POOL_HOST_LIMIT ((size_t) 256 << 20)
+#define POOL_DEV_LIMIT ((size_t) 1 << 30)
 
 typedef struct {
-  void* host[MAX_SCRATCH];
-  void* dev[MAX_SCRATCH];
-  int nhost, ndev;
+  void* p;
+  size_t n;
+  int dev;
+} pooled;
+
+static pthread_mutex_t pool_mu = PTHREAD_MUTEX_INITIALIZER;
+static pooled pool[POOL_MAX];
+static int npool;
+static size_t pool_bytes[2]; /* host, device */
+static hipStream_t pool_stream;
+
+static int cache_on(void) {
+  const char* v = getenv("REDSET_HIP_SCRATCH_CACHE");
+  return !v || atoi(v) != 0;
+}
+
+typedef struct {
+  pooled buf[2 * MAX_SCRATCH];
+  int nbuf;
   hipStream_t stream;
   int rc;
 } scratch;
 
 static void scratch_init(scratch* S) {
   memset(S, 0, sizeof(*S));
-  if (hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (cache_on()) {
+    pthread_mutex_lock(&pool_mu);
+    S->stream = pool_stream;
+    pool_stream = NULL;
+    pthread_mutex_unlock(&pool_mu);
+  }
+  if (!S->stream && hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) != hipSuccess) {
     S->stream = NULL;
     S->rc = fail("hipStreamCreate failed");
   }
 }
 
-static uint8_t* scratch_host(scratch* S, size_t n) {
+/* the smallest cached buffer of the kind that holds n bytes, or a new one */
+static uint8_t* scratch_get(scratch* S, size_t n, int dev) {
   void* p = NULL;
-  if (S->rc || S->nhost == MAX_SCRATCH) return NULL;
-  if (hipHostMalloc(&p, n ? n : 1, hipHostMallocDefault) != hipSuccess) {
-    S->rc = fail("hipHostMalloc(%zu) failed", n);
-    return NULL;
+  if (S->rc || S->nbuf == 2 * MAX_SCRATCH) return NULL;
+  if (n == 0) n = 1;
+  size_t have = 0;
+  if (cache_on()) {
+    pthread_mutex_lock(&pool_mu);
+    int best = -1;
+    for (int i = 0; i < npool; ++i)
+      if (pool[i].dev == dev && pool[i].n >= n && (best < 0 || pool[i].n < pool[best].n)) best = i;
+    if (best >= 0) {
+      p = pool[best].p;
+      have = pool[best].n;
+      pool_bytes[dev] -= have;
+      pool[best] = pool[--npool];
+    }
+    pthread_mutex_unlock(&pool_mu);
   }
-  S->host[S->nhost++] = p;
+  if (!p) {
+    if ((dev ? hipMalloc(&p, n) : hipHostMalloc(&p, n, hipHostMallocDefault)) != hipSuccess) {
+      S->rc = fail("%s(%zu) failed", dev ? "hipMalloc" : "hipHostMalloc", n);
+      return NULL;
+    }
+    have = n;
+  }
+  S->buf[S->nbuf].p = p;
+  S->buf[S->nbuf].n = have;
+  S->buf[S->nbuf].dev = dev;
+  ++S->nbuf;
   return (uint8_t*) p;
 }
 
-static uint8_t* scratch_dev(scratch* S, size_t n) {
-  void* p = NULL;
-  if (S->rc || S->ndev == MAX_SCRATCH) return NULL;
-  if (hipMalloc(&p, n ? n : 1) != hipSuccess) {
-    S->rc = fail("hipMalloc(%zu) failed", n);
-    return NULL;
-  }
-  S->dev[S->ndev++] = p;
-  return (uint8_t*) p;
+static uint8_t* scratch_host(scratch* S, size_t n) { return scratch_get(S, n, 0); }
+static uint8_t* scratch_dev(scratch* S, size_t n) { return scratch_get(S, n, 1); }
+
+static void release(const pooled* b) {
+  if (b->dev) (void) hipFree(b->p);
+  else (void) hipHostFree(b->p);
 }
 
-static void scratch_free(scratch* S) {
-  if (S->stream) (void) hipStreamSynchronize(S->stream);
-  for (int i = 0; i < S->nhost; ++i) (void) hipHostFree(S->host[i]);
-  for (int i = 0; i < S->ndev; ++i) (void) hipFree(S->dev[i]);
+/* ok: the call succeeded, its scratch may be cached */
+static void scratch_free(scratch* S, int ok) {
+  if (S->stream && hipStreamSynchronize(S->stream) != hipSuccess) ok = 0;
+  ok = ok && cache_on();
+  pthread_mutex_lock(&pool_mu);
+  for (int i = 0; i < S->nbuf; ++i) {
+    const pooled* b = &S->buf[i];
+    const size_t limit = b->dev ? POOL_DEV_LIMIT : POOL_HOST_LIMIT;
+    if (ok && npool < POOL_MAX && pool_bytes[b->dev] + b->n <= limit) {
+      pool[npool++] = *b;
+      pool_bytes[b->dev] += b->n;
+    } else {
+      release(b);
+    }
+  }
+  if (S->stream && ok && !pool_stream) {
+    pool_stream = S->stream;
+    S->stream = NULL;
+  }
+  pthread_mutex_unlock(&pool_mu);
   if (S->stream) (void) hipStreamDestroy(S->stream);
+  S->stream = NULL;
+  S->nbuf = 0;
+}
+
+void redset_hip_rank_scratch_release(void) {
+  pthread_mutex_lock(&pool_mu);
+  for (int i = 0; i < npool; ++i) release(&pool[i]);
+  npool = 0;
+  pool_bytes[0] = pool_bytes[1] = 0;
+  if (pool_stream) (void) hipStreamDestroy(pool_stream);
+  pool_stream = NULL;
+  pthread_mutex_unlock(&pool_mu);
 }
 
 static int h2d(scratch* S, void* dst, const void* src, size_t n) {
@@ -321,7 +404,7 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
     }
   }
 out:
-  scratch_free(&S);
+  scratch_free(&S, rc == 0);
   for (int k = 0; k < 2; ++k) {
     if (ev_recv[k]) (void) hipEventDestroy(ev_recv[k]);
     if (ev_par[k]) (void) hipEventDestroy(ev_par[k]);
@@ -479,7 +562,7 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
     prev_count = count;
   }
 out:
-  scratch_free(&S);
+  scratch_free(&S, rc == 0);
   for (int k = 0; k < 2; ++k)
     if (ev_done[k]) (void) hipEventDestroy(ev_done[k]);
   free(D);
@@ -578,7 +661,7 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
     prev_count = count;
   }
 out:
-  scratch_free(&S);
+  scratch_free(&S, rc == 0);
   for (int k = 0; k < 2; ++k)
     if (ev_done[k]) (void) hipEventDestroy(ev_done[k]);
   free(ins);
@@ -687,7 +770,7 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
     }
   }
 out:
-  scratch_free(&S);
+  scratch_free(&S, rc == 0);
   for (int k = 0; k < 2; ++k)
     if (ev_done[k]) (void) hipEventDestroy(ev_done[k]);
   free(ins);

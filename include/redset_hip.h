@@ -191,6 +191,12 @@ int redset_hip_xor_rebuild_stream(int ranks, int root, size_t chunk_size, int fi
                                   size_t slice_bytes, int io_threads, const redset_hip_io* io,
                                   redset_hip_stream_stats* stats);
 
+/* The streaming calls keep a successful call's three streams and (up to
+ * 256 MiB pinned, 1 GiB of device memory) its staging buffers for the next
+ * call; REDSET_HIP_SCRATCH_CACHE=0 allocates and frees per call. This frees
+ * what is cached. */
+void redset_hip_release_scratch(void);
+
 /* Built-in I/O over host memory laid out like the device set layout
  * (lofi[r] + s*cell_stride, parity[r] + i*cell_stride). pinned != 0 declares
  * the memory page-locked (hipHostMalloc / hipHostRegister): cells are then

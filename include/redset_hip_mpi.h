@@ -54,7 +54,8 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
  * buffers and stream for the next call (at most 256 MiB pinned, 1 GiB of
  * device memory); REDSET_HIP_SCRATCH_CACHE=0 allocates and frees per call
  * instead, as the reference does (src/redset_reedsolomon.c:298-302, :397-399).
- * This frees the cache, e.g. from redset_finalize. */
+ * This frees the cache (and redset_hip_release_scratch's), e.g. from
+ * redset_finalize. */
 void redset_hip_rank_scratch_release(void);
 
 /* Transport of the sharded path (redset_hip_rs_sharded_plan) over MPI

@@ -50,6 +50,7 @@ EXPORTED_SYMBOLS = (
     "redset_hip_xor_rebuild_stream",
     "redset_hip_hostio_create",
     "redset_hip_hostio_destroy",
+    "redset_hip_release_scratch",
     "redset_hip_fileio_create",
     "redset_hip_fileio_destroy",
     "redset_hip_shard_slice_bytes",
@@ -198,6 +199,7 @@ _SIGNATURES = {
     "redset_hip_xor_rebuild_stream": (c_int, [c_int, c_int, c_size_t, c_int, c_int, c_size_t, c_int, _IOP, _STP]),
     "redset_hip_hostio_create": (c_int, [c_int, _PP, _PP, c_size_t, c_int, _IOP, POINTER(c_void_p)]),
     "redset_hip_hostio_destroy": (None, [c_void_p]),
+    "redset_hip_release_scratch": (None, []),
     "redset_hip_fileio_create": (
         c_int,
         [c_int, POINTER(c_int), POINTER(c_char_p), POINTER(c_ulonglong), POINTER(c_char_p), POINTER(c_ulonglong),

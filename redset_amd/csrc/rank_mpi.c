@@ -168,6 +168,7 @@ void redset_hip_rank_scratch_release(void) {
   if (pool_stream) (void) hipStreamDestroy(pool_stream);
   pool_stream = NULL;
   pthread_mutex_unlock(&pool_mu);
+  redset_hip_release_scratch(); /* the streaming pipeline's cache too */
 }
 
 static int h2d(scratch* S, void* dst, const void* src, size_t n) {

@@ -45,6 +45,106 @@ double now_s() {
   return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Streams and staging buffers kept across calls. Creating and destroying a
+// stream costs ~2.7 ms and pinning ~0.15 ms per MiB each way
+// (profiles/r02_alloc_probe.jsonl): for a small set that was a third of the
+// call. A successful call hands its three streams and (within the limits)
+// its slot buffers back; REDSET_HIP_SCRATCH_CACHE=0 allocates and frees per
+// call; redset_hip_release_scratch() empties the cache.
+class ResourceCache {
+ public:
+  static ResourceCache& get() {
+    static ResourceCache c;
+    return c;
+  }
+  static bool enabled() {
+    const char* v = std::getenv("REDSET_HIP_SCRATCH_CACHE");
+    return !v || std::atoi(v) != 0;
+  }
+  hipStream_t take_stream() {
+    if (enabled()) {
+      std::lock_guard<std::mutex> g(mu_);
+      if (!streams_.empty()) {
+        hipStream_t s = streams_.back();
+        streams_.pop_back();
+        return s;
+      }
+    }
+    hipStream_t s = nullptr;
+    if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    return s;
+  }
+  void give_stream(hipStream_t s, bool ok) {
+    if (!s) return;
+    if (ok && enabled()) {
+      std::lock_guard<std::mutex> g(mu_);
+      if (streams_.size() < 6) {
+        streams_.push_back(s);
+        return;
+      }
+    }
+    (void) hipStreamDestroy(s);
+  }
+  // the smallest cached buffer of the kind holding n bytes, or a new one;
+  // *have = its size
+  void* take_buf(size_t n, bool dev, size_t* have) {
+    if (n == 0) n = 1;
+    if (enabled()) {
+      std::lock_guard<std::mutex> g(mu_);
+      int best = -1;
+      for (int i = 0; i < static_cast<int>(bufs_.size()); ++i)
+        if (bufs_[i].dev == dev && bufs_[i].n >= n && (best < 0 || bufs_[i].n < bufs_[best].n)) best = i;
+      if (best >= 0) {
+        Buf b = bufs_[best];
+        bufs_.erase(bufs_.begin() + best);
+        bytes_[dev] -= b.n;
+        *have = b.n;
+        return b.p;
+      }
+    }
+    void* p = nullptr;
+    if ((dev ? hipMalloc(&p, n) : hipHostMalloc(&p, n, hipHostMallocDefault)) != hipSuccess) return nullptr;
+    *have = n;
+    return p;
+  }
+  void give_buf(void* p, size_t n, bool dev, bool ok) {
+    if (!p) return;
+    if (ok && enabled()) {
+      std::lock_guard<std::mutex> g(mu_);
+      const size_t limit = dev ? (size_t(1) << 30) : (size_t(256) << 20);
+      if (bufs_.size() < 32 && bytes_[dev] + n <= limit) {
+        bufs_.push_back(Buf{p, n, dev});
+        bytes_[dev] += n;
+        return;
+      }
+    }
+    free_buf(p, dev);
+  }
+  void release() {
+    std::lock_guard<std::mutex> g(mu_);
+    for (const Buf& b : bufs_) free_buf(b.p, b.dev);
+    bufs_.clear();
+    bytes_[0] = bytes_[1] = 0;
+    for (hipStream_t s : streams_) (void) hipStreamDestroy(s);
+    streams_.clear();
+  }
+
+ private:
+  struct Buf {
+    void* p;
+    size_t n;
+    bool dev;
+  };
+  static void free_buf(void* p, bool dev) {
+    if (dev) (void) hipFree(p);
+    else (void) hipHostFree(p);
+  }
+  std::mutex mu_;
+  std::vector<Buf> bufs_;
+  size_t bytes_[2] = {0, 0};
+  std::vector<hipStream_t> streams_;
+};
+
 // Fixed pool of I/O workers; run() executes a batch and waits for it.
 class IoPool {
  public:
@@ -116,6 +216,7 @@ struct Slot {
   uint8_t* h_out = nullptr;
   uint8_t* d_in = nullptr;
   uint8_t* d_out = nullptr;
+  size_t n_h_in = 0, n_h_out = 0, n_d_in = 0, n_d_out = 0;  // sizes as allocated (cached ones may be larger)
   hipEvent_t ev_in = nullptr, ev_comp = nullptr, ev_done = nullptr, ev_start = nullptr;
   SlotState state = kFree;
   size_t unit = 0;
@@ -165,9 +266,10 @@ int try_zero_copy(const std::vector<StripeMap>& maps, size_t chunk, const redset
     }
   }
   const double t0 = now_s();
-  hipStream_t s = nullptr;
+  ResourceCache& cache = ResourceCache::get();
+  hipStream_t s = cache.take_stream();
   hipEvent_t e0 = nullptr, e1 = nullptr;
-  int rc = hip_ok(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "stream");
+  int rc = s ? 0 : fail("hipStreamCreate failed");
   rc = rc ? rc : hip_ok(hipEventCreate(&e0), "event");
   rc = rc ? rc : hip_ok(hipEventCreate(&e1), "event");
   rc = rc ? rc : hip_ok(hipEventRecord(e0, s), "event record");
@@ -182,10 +284,10 @@ int try_zero_copy(const std::vector<StripeMap>& maps, size_t chunk, const redset
   rc = rc ? rc : hip_ok(hipStreamSynchronize(s), "stream synchronize");
   float ms = 0;
   if (rc == 0 && hipEventElapsedTime(&ms, e0, e1) == hipSuccess) st->gpu_seconds = ms * 1e-3;
-  if (s) (void) hipStreamSynchronize(s);
+  const bool synced = s && hipStreamSynchronize(s) == hipSuccess;
   if (e0) (void) hipEventDestroy(e0);
   if (e1) (void) hipEventDestroy(e1);
-  if (s) (void) hipStreamDestroy(s);
+  cache.give_stream(s, rc == 0 && synced);
   st->seconds = now_s() - t0;
   *rc_out = rc;
   return 0;
@@ -227,16 +329,19 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
   }
 
   Slot slots[kSlots];
-  hipStream_t s_in = nullptr, s_comp = nullptr, s_out = nullptr;
-  int rc = 0;
-  rc = rc ? rc : hip_ok(hipStreamCreateWithFlags(&s_in, hipStreamNonBlocking), "stream");
-  rc = rc ? rc : hip_ok(hipStreamCreateWithFlags(&s_comp, hipStreamNonBlocking), "stream");
-  rc = rc ? rc : hip_ok(hipStreamCreateWithFlags(&s_out, hipStreamNonBlocking), "stream");
+  ResourceCache& cache = ResourceCache::get();
+  hipStream_t s_in = cache.take_stream(), s_comp = cache.take_stream(), s_out = cache.take_stream();
+  int rc = (s_in && s_comp && s_out) ? 0 : fail("hipStreamCreate failed");
+  auto buf = [&](uint8_t** p, size_t* have, size_t n, bool dev) {
+    if (rc) return;
+    *p = static_cast<uint8_t*>(cache.take_buf(n, dev, have));
+    if (!*p) rc = fail("%s(%zu) failed", dev ? "hipMalloc" : "hipHostMalloc", n);
+  };
   for (Slot& S : slots) {
-    rc = rc ? rc : hip_ok(hipHostMalloc(reinterpret_cast<void**>(&S.h_in), max_in * slice, hipHostMallocDefault), "hipHostMalloc");
-    rc = rc ? rc : hip_ok(hipHostMalloc(reinterpret_cast<void**>(&S.h_out), max_out * slice, hipHostMallocDefault), "hipHostMalloc");
-    rc = rc ? rc : hip_ok(hipMalloc(reinterpret_cast<void**>(&S.d_in), max_in * slice), "hipMalloc");
-    rc = rc ? rc : hip_ok(hipMalloc(reinterpret_cast<void**>(&S.d_out), max_out * slice), "hipMalloc");
+    buf(&S.h_in, &S.n_h_in, max_in * slice, false);
+    buf(&S.h_out, &S.n_h_out, max_out * slice, false);
+    buf(&S.d_in, &S.n_d_in, max_in * slice, true);
+    buf(&S.d_out, &S.n_d_out, max_out * slice, true);
     rc = rc ? rc : hip_ok(hipEventCreateWithFlags(&S.ev_in, hipEventDisableTiming), "event");
     rc = rc ? rc : hip_ok(hipEventCreateWithFlags(&S.ev_comp, hipEventDisableTiming), "event");
     rc = rc ? rc : hip_ok(hipEventCreate(&S.ev_start), "event");
@@ -379,22 +484,22 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
     reader.join();
     writer.join();
   }
-  (void) hipStreamSynchronize(s_in);
-  (void) hipStreamSynchronize(s_comp);
-  (void) hipStreamSynchronize(s_out);
+  bool ok = rc == 0 && io_err.load() != 2;
+  for (hipStream_t s : {s_in, s_comp, s_out})
+    if (s && hipStreamSynchronize(s) != hipSuccess) ok = false;
   for (Slot& S : slots) {
-    if (S.h_in) (void) hipHostFree(S.h_in);
-    if (S.h_out) (void) hipHostFree(S.h_out);
-    if (S.d_in) (void) hipFree(S.d_in);
-    if (S.d_out) (void) hipFree(S.d_out);
+    cache.give_buf(S.h_in, S.n_h_in, false, ok);
+    cache.give_buf(S.h_out, S.n_h_out, false, ok);
+    cache.give_buf(S.d_in, S.n_d_in, true, ok);
+    cache.give_buf(S.d_out, S.n_d_out, true, ok);
     if (S.ev_in) (void) hipEventDestroy(S.ev_in);
     if (S.ev_comp) (void) hipEventDestroy(S.ev_comp);
     if (S.ev_start) (void) hipEventDestroy(S.ev_start);
     if (S.ev_done) (void) hipEventDestroy(S.ev_done);
   }
-  if (s_in) (void) hipStreamDestroy(s_in);
-  if (s_comp) (void) hipStreamDestroy(s_comp);
-  if (s_out) (void) hipStreamDestroy(s_out);
+  cache.give_stream(s_in, ok);
+  cache.give_stream(s_comp, ok);
+  cache.give_stream(s_out, ok);
   st.seconds = now_s() - t0;
   st.read_seconds = read_ns.load() * 1e-9;
   st.write_seconds = write_ns.load() * 1e-9;
@@ -548,6 +653,9 @@ int fileio_write(void* ctx, int rank, int kind, int index, unsigned long long of
 }  // namespace
 
 extern "C" {
+
+void redset_hip_release_scratch(void) { ResourceCache::get().release(); }
+
 
 int redset_hip_rs_encode_stream(const redset_hip_rs* rs, size_t chunk_size, int first_stripe, int nstripes,
                                 size_t slice_bytes, int io_threads, const redset_hip_io* io,

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Host-code AddressSanitizer on the GPU box: the offline rebuild tool (the
+# Host-code AddressSanitizer (then ThreadSanitizer) on the GPU box: the offline rebuild tool (the
 # streaming pipeline + file I/O), the per-rank MPI backends and the sharded
 # driver, built by tests/asan/Makefile with -Xarch_host ASan only (no GPU
 # instrumentation), driven by their own GPU tests.
@@ -20,4 +20,13 @@ timeout -k 10 600 python -u -m pytest -x -v --timeout 100 --timeout-method threa
 s=$?
 tail -5 "$OUT/asan_tests.log"
 grep -c "AddressSanitizer\|LeakSanitizer" "$OUT/asan_tests.log" || true
+[ $s -eq 0 ] || exit $s
+# ThreadSanitizer (make -C tests/asan SANITIZER=thread B=build_tsan): the
+# offline tool's streaming pipeline -- reader, writer, I/O pool and feeder
+# threads -- with the uninstrumented ROCm runtime's interceptors suppressed
+export TSAN_OPTIONS="halt_on_error=0:exitcode=66:report_signal_unsafe=0:suppressions=$PWD/tests/asan/tsan.supp"
+REDSET_HIP_REBUILD_TOOL=$PWD/tests/asan/build_tsan/redset_hip_rebuild timeout -k 10 400 python -u -m pytest -x -v \
+  --timeout 100 --timeout-method thread tests/test_gpu_rebuild_tool.py > "$OUT/tsan_tests.log" 2>&1
+s=$?
+tail -3 "$OUT/tsan_tests.log"
 exit $s

@@ -285,13 +285,13 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
   unsigned char* mat = malloc((size_t) (p + e) * p);
   unsigned char* coef = malloc((size_t) e * d);       /* [slot i][ring step s] */
   const unsigned char** ins = malloc(sizeof(*ins) * (size_t) G);
-  MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) e);
+  MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) e * (size_t) G);
   scratch S;
   scratch_init(&S);
   /* two of everything the GPU touches: window w+1's exchange fills one
    * receive buffer while the GPU copies and combines window w from the other,
    * and slice n's parity is written while slice n+1 is exchanged */
-  uint8_t* h_send = scratch_host(&S, B);
+  uint8_t* h_send = scratch_host(&S, (size_t) G * B); /* the window's own segments, one per step */
   uint8_t* h_recv[2] = {scratch_host(&S, (size_t) G * e * B), scratch_host(&S, (size_t) G * e * B)};
   uint8_t* h_par[2] = {scratch_host(&S, (size_t) e * B), scratch_host(&S, (size_t) e * B)};
   uint8_t* d_recv[2] = {scratch_dev(&S, (size_t) G * e * B), scratch_dev(&S, (size_t) G * e * B)};
@@ -333,23 +333,34 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
         rc = REDSET_FAILURE;
         dev_failed = 1;
       }
-      for (int s = s0; s < s0 + gs; ++s) { /* chunk_step = p-1 .. e, src/redset_reedsolomon.c:329-377 */
-        const int step = p - 1 - s;
-        const int chunk_id = (r + step) % p;
+      /* the window's steps (chunk_step = p-1 .. e, src/redset_reedsolomon.c:
+       * 329-377) exchanged together: at step s this rank sends its segment of
+       * stripe r + chunk_step to the e parity holders of that stripe and
+       * receives, for each of its own parity slots, one segment of stripe
+       * r - ... (the same pairs as the reference's ring, which forwards
+       * partial sums instead). Tag = step within the window, so a pair that
+       * meets at several steps matches them one to one. */
+      for (int s = s0; s < s0 + gs; ++s) {
+        const int chunk_id = (r + p - 1 - s) % p;
         const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
-        if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0) {
+        uint8_t* mine = h_send + (size_t) (s - s0) * B;
+        if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, mine) != 0) {
           rc = fail("lofi read failed");
-          memset(h_send, 0, count);
+          memset(mine, 0, count);
         }
-        int k = 0;
+      }
+      int k = 0;
+      for (int s = s0; s < s0 + gs; ++s) {
+        const int step = p - 1 - s;
         for (int i = 0; i < e; ++i) {
           const int dist = p - step + i;
-          MPI_Irecv(h_recv[bb] + ((size_t) (s - s0) * e + i) * B, (int) count, MPI_BYTE, (r + dist) % p, 0, comm,
+          MPI_Irecv(h_recv[bb] + ((size_t) (s - s0) * e + i) * B, (int) count, MPI_BYTE, (r + dist) % p, s - s0,
+                    comm, &req[k++]);
+          MPI_Isend(h_send + (size_t) (s - s0) * B, (int) count, MPI_BYTE, (r - dist + p) % p, s - s0, comm,
                     &req[k++]);
-          MPI_Isend(h_send, (int) count, MPI_BYTE, (r - dist + p) % p, 0, comm, &req[k++]);
         }
-        MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
       }
+      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
       ++wcount;
       if (dev_failed) continue;
       /* the window's gs*e slices: one H2D, one kernel per slot accumulating
@@ -445,20 +456,29 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   scratch_init(&S);
   /* two sets of slice buffers: slice n's ring exchange and GPU solve overlap
    * slice n-1's gather to the erased members and its writes */
-  uint8_t* h_send = scratch_host(&S, B);
+  uint8_t* h_send = scratch_host(&S, (size_t) p * B); /* my cell of stripe c, for solver c */
   uint8_t* h_cells[2] = {scratch_host(&S, (size_t) p * B), scratch_host(&S, (size_t) p * B)};
   uint8_t* h_out[2] = {scratch_host(&S, (size_t) missing * B), scratch_host(&S, (size_t) missing * B)};
   uint8_t* h_gather = scratch_host(&S, (size_t) p * B); /* rebuilt cells from every solver */
+  unsigned char* send_to = calloc((size_t) p, 1);    /* solver c's decode reads my cell of stripe c */
+  unsigned char* Dc = malloc((size_t) missing * p);
   uint8_t* d_cells[2] = {scratch_dev(&S, (size_t) p * B), scratch_dev(&S, (size_t) p * B)};
   uint8_t* d_out[2] = {scratch_dev(&S, (size_t) missing * B), scratch_dev(&S, (size_t) missing * B)};
   hipEvent_t ev_done[2] = {NULL, NULL};
   int rc = S.rc ? S.rc : hrc;
   for (int k = 0; k < 2 && !rc; ++k)
     if (hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
-  if (!rc && (!D || !coef || !cols || !ins || !outs || !req)) rc = fail("out of host memory");
+  if (!rc && (!D || !coef || !cols || !ins || !outs || !req || !send_to || !Dc)) rc = fail("out of host memory");
   /* member r solves stripe r (decode_chunk_id = rank, :607-611): one linear
    * map equal to redset_rs_reduce_decode + redset_rs_gaussian_solve */
   if (!rc) rc = redset_hip_rs_decode_matrix(rs, missing, rebuild_ranks, r, D);
+  /* every member derives every stripe's map the same way, so it knows which
+   * solvers read its cells: the erased members' cells, and survivors' cells a
+   * map does not use, are never sent (the reference's ring forwards them all) */
+  for (int c = 0; c < p && !rc; ++c) {
+    rc = redset_hip_rs_decode_matrix(rs, missing, rebuild_ranks, c, Dc);
+    for (int i = 0; i < missing && !rc; ++i) send_to[c] |= Dc[(size_t) i * p + r] != 0;
+  }
   if ((rc = agree_setup(comm, rc))) goto out;
   int ncols = 0;
   for (int s = 0; s < p; ++s) {
@@ -481,33 +501,34 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
     const size_t count = more ? min_sz(B, chunk_size - nread) : 0;
     const int bb = (int) (n & 1);
     if (more) {
-      for (int step = 0; step < p; ++step) { /* :646-703 */
-        const int lhs = (r - step + p) % p, rhs = (r + step) % p;
-        const int chunk_id = (r + step) % p;
-        const int enc = redset_hip_rs_get_encoding_id(p, e, r, chunk_id);
-        if (!need_rebuild) {
-          int bad;
-          if (enc < p) {
-            const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
-            bad = lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, h_send) != 0;
-            if (bad) rc = fail("lofi read failed");
-          } else {
-            const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) nread;
-            bad = pread_full(fd_chunk, h_send, count, off) != 0;
-            if (bad) rc = fail("read %s failed", chunk_file);
-          }
-          if (bad) memset(h_send, 0, count);
+      /* the slice's cells straight to their solvers, all at once (the
+       * reference passes them round a ring, one step at a time, :646-703):
+       * my cell of stripe c to member c, stripe r's used cells to me */
+      for (int c = 0; c < p; ++c) {
+        if (!send_to[c]) continue;
+        uint8_t* mine = h_send + (size_t) c * B;
+        const int enc = redset_hip_rs_get_encoding_id(p, e, r, c);
+        int bad;
+        if (enc < p) {
+          const int seg = redset_hip_rs_get_data_id(p, e, r, c);
+          bad = lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, mine) != 0;
+          if (bad) rc = fail("lofi read failed");
         } else {
-          memset(h_send, 0, count); /* an erased member contributes nothing */
+          const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) nread;
+          bad = pread_full(fd_chunk, mine, count, off) != 0;
+          if (bad) rc = fail("read %s failed", chunk_file);
         }
-        if (step > 0) {
-          MPI_Irecv(h_cells[bb] + (size_t) lhs * B, (int) count, MPI_BYTE, lhs, TAG_RING, comm, &req[0]);
-          MPI_Isend(h_send, (int) count, MPI_BYTE, rhs, TAG_RING, comm, &req[1]);
-          MPI_Waitall(2, req, MPI_STATUSES_IGNORE);
-        } else {
-          memcpy(h_cells[bb] + (size_t) r * B, h_send, count);
-        }
+        if (bad) memset(mine, 0, count);
       }
+      int k = 0;
+      for (int j = 0; j < ncols; ++j)
+        if (cols[j] != r)
+          MPI_Irecv(h_cells[bb] + (size_t) cols[j] * B, (int) count, MPI_BYTE, cols[j], TAG_RING, comm, &req[k++]);
+      for (int c = 0; c < p; ++c)
+        if (c != r && send_to[c])
+          MPI_Isend(h_send + (size_t) c * B, (int) count, MPI_BYTE, c, TAG_RING, comm, &req[k++]);
+      if (send_to[r]) memcpy(h_cells[bb] + (size_t) r * B, h_send + (size_t) r * B, count);
+      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
       /* enqueue this slice's solve; it runs while the previous slice is gathered */
       if (!dev_failed) {
         for (int k = 0; k < ncols; ++k) ins[k] = d_cells[bb] + (size_t) cols[k] * B;
@@ -569,6 +590,8 @@ out:
   free(D);
   free(coef);
   free(cols);
+  free(send_to);
+  free(Dc);
   free(ins);
   free(outs);
   free(req);

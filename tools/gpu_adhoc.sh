@@ -1,13 +1,1 @@
-set -o pipefail
-cd "${GRAFT_REPO_ROOT}"
-export TMPDIR=/tmp
-O=gpurun_out/r02s35
-mkdir -p $O
-timeout -k 10 400 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_gpu_mpi.py > $O/tests.log 2>&1 || { tail -30 $O/tests.log; exit 1; }
-tail -2 $O/tests.log
-bash tools/gpu_asan.sh r02s35_san || exit 2
-for ch in 16 64; do
-timeout -k 10 400 python -u tools/rank_bench.py --scheme rs --ranks 11 --encoding 3 --chunk-mib $ch --repeat 3 >> $O/rank.jsonl || exit 3
-done
-timeout -k 10 300 python -u tools/rank_bench.py --scheme rs --ranks 11 --encoding 3 --chunk-mib 16 --repeat 3 --lost 0,5,9 >> $O/rank.jsonl || exit 4
-cat $O/rank.jsonl
+bash tools/gpu_session.sh r02s36

@@ -230,3 +230,44 @@ def test_mpi_sharded_gpu_random(seed):
     res = run_group(cmd, 120, env={**os.environ, "SHARDED_TEST_SEED": str(seed)})
     assert res.returncode == 0, (np_, p, e, chunk, lost, res.stdout + res.stderr)
     assert res.stdout.count("rebuild gather") == np_
+
+
+@pytest.mark.parametrize("scheme,p,e,lost", [("rs", 6, 2, [1, 4]), ("xor", 5, 1, [3])])
+def test_mpi_rank_backends_repeated_calls(oracle, tmp_path, scheme, p, e, lost):
+    """Three backend calls per process (RANK_TEST_REPEAT=3): the second and
+    third run on the scratch and stream the first left in the process-wide
+    cache (dirty buffers), and must write the same bytes."""
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    tmp = str(tmp_path)
+    d = p - e
+    rng = np.random.default_rng(77 + p)
+    files, chunk = _setup(tmp, p, d, rng, 400_000)
+    header = [256] * p
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, header, reds)
+    crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
+    env = {**os.environ, "RANK_TEST_REPEAT": "3"}
+    cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST, scheme, "encode", str(e), tmp, "32768"]
+    res = run_group(cmd, 120, env=env)
+    assert res.returncode == 0 and "call 3 of 3" in res.stdout, res.stdout + res.stderr
+    lofi = [_logical(fl, d * chunk) for fl in files]
+    want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+    if scheme == "rs":
+        oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    else:
+        oracle.xor_encode_set(p, lofi, want, chunk)
+    for r in range(p):
+        assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[256:], want[r]), r
+    for r in lost:
+        for path, _ in files[r]:
+            os.unlink(path)
+        os.unlink(reds[r])
+    cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST, scheme, "rebuild", str(e), tmp, "32768"] + \
+        [str(x) for x in lost]
+    res = run_group(cmd, 120, env=env)
+    assert res.returncode == 0 and "call 3 of 3" in res.stdout, res.stdout + res.stderr
+    for r in lost:
+        for path, _ in files[r]:
+            assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
+        assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[256:256 + e * chunk], want[r]), r

@@ -59,7 +59,8 @@ static size_t min_sz(size_t a, size_t b) { return a < b ? a : b; }
 typedef struct {
   void* p;
   size_t n;
-  int dev;
+  int dev;    /* device memory (else pinned host) */
+  int device; /* current device when it was made: handed out only to calls on it */
 } pooled;
 
 static pthread_mutex_t pool_mu = PTHREAD_MUTEX_INITIALIZER;
@@ -67,6 +68,12 @@ static pooled pool[POOL_MAX];
 static int npool;
 static size_t pool_bytes[2]; /* host, device */
 static hipStream_t pool_stream;
+static int pool_stream_device = -1;
+
+static int current_device(void) {
+  int d = -1;
+  return hipGetDevice(&d) == hipSuccess ? d : -1;
+}
 
 static int cache_on(void) {
   const char* v = getenv("REDSET_HIP_SCRATCH_CACHE");
@@ -77,15 +84,19 @@ typedef struct {
   pooled buf[2 * MAX_SCRATCH];
   int nbuf;
   hipStream_t stream;
+  int device;
   int rc;
 } scratch;
 
 static void scratch_init(scratch* S) {
   memset(S, 0, sizeof(*S));
+  S->device = current_device();
   if (cache_on()) {
     pthread_mutex_lock(&pool_mu);
-    S->stream = pool_stream;
-    pool_stream = NULL;
+    if (pool_stream && pool_stream_device == S->device) {
+      S->stream = pool_stream;
+      pool_stream = NULL;
+    }
     pthread_mutex_unlock(&pool_mu);
   }
   if (!S->stream && hipStreamCreateWithFlags(&S->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -104,7 +115,8 @@ static uint8_t* scratch_get(scratch* S, size_t n, int dev) {
     pthread_mutex_lock(&pool_mu);
     int best = -1;
     for (int i = 0; i < npool; ++i)
-      if (pool[i].dev == dev && pool[i].n >= n && (best < 0 || pool[i].n < pool[best].n)) best = i;
+      if (pool[i].dev == dev && pool[i].device == S->device && pool[i].n >= n && (best < 0 || pool[i].n < pool[best].n))
+        best = i;
     if (best >= 0) {
       p = pool[best].p;
       have = pool[best].n;
@@ -123,6 +135,7 @@ static uint8_t* scratch_get(scratch* S, size_t n, int dev) {
   S->buf[S->nbuf].p = p;
   S->buf[S->nbuf].n = have;
   S->buf[S->nbuf].dev = dev;
+  S->buf[S->nbuf].device = S->device;
   ++S->nbuf;
   return (uint8_t*) p;
 }
@@ -152,6 +165,7 @@ static void scratch_free(scratch* S, int ok) {
   }
   if (S->stream && ok && !pool_stream) {
     pool_stream = S->stream;
+    pool_stream_device = S->device;
     S->stream = NULL;
   }
   pthread_mutex_unlock(&pool_mu);

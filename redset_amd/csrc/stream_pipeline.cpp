@@ -61,14 +61,22 @@ class ResourceCache {
     const char* v = std::getenv("REDSET_HIP_SCRATCH_CACHE");
     return !v || std::atoi(v) != 0;
   }
+  // Everything cached belongs to the device that was current when it was
+  // made, and is handed out again only while that device is current.
+  static int device() {
+    int d = -1;
+    return hipGetDevice(&d) == hipSuccess ? d : -1;
+  }
   hipStream_t take_stream() {
     if (enabled()) {
+      const int dev = device();
       std::lock_guard<std::mutex> g(mu_);
-      if (!streams_.empty()) {
-        hipStream_t s = streams_.back();
-        streams_.pop_back();
-        return s;
-      }
+      for (size_t i = 0; i < streams_.size(); ++i)
+        if (streams_[i].device == dev) {
+          hipStream_t s = streams_[i].s;
+          streams_.erase(streams_.begin() + static_cast<long>(i));
+          return s;
+        }
     }
     hipStream_t s = nullptr;
     if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) return nullptr;
@@ -77,9 +85,10 @@ class ResourceCache {
   void give_stream(hipStream_t s, bool ok) {
     if (!s) return;
     if (ok && enabled()) {
+      const int dev = device();
       std::lock_guard<std::mutex> g(mu_);
       if (streams_.size() < 6) {
-        streams_.push_back(s);
+        streams_.push_back(CachedStream{s, dev});
         return;
       }
     }
@@ -90,10 +99,12 @@ class ResourceCache {
   void* take_buf(size_t n, bool dev, size_t* have) {
     if (n == 0) n = 1;
     if (enabled()) {
+      const int cur = device();
       std::lock_guard<std::mutex> g(mu_);
       int best = -1;
       for (int i = 0; i < static_cast<int>(bufs_.size()); ++i)
-        if (bufs_[i].dev == dev && bufs_[i].n >= n && (best < 0 || bufs_[i].n < bufs_[best].n)) best = i;
+        if (bufs_[i].dev == dev && bufs_[i].device == cur && bufs_[i].n >= n && (best < 0 || bufs_[i].n < bufs_[best].n))
+          best = i;
       if (best >= 0) {
         Buf b = bufs_[best];
         bufs_.erase(bufs_.begin() + best);
@@ -110,10 +121,11 @@ class ResourceCache {
   void give_buf(void* p, size_t n, bool dev, bool ok) {
     if (!p) return;
     if (ok && enabled()) {
+      const int cur = device();
       std::lock_guard<std::mutex> g(mu_);
       const size_t limit = dev ? (size_t(1) << 30) : (size_t(256) << 20);
       if (bufs_.size() < 32 && bytes_[dev] + n <= limit) {
-        bufs_.push_back(Buf{p, n, dev});
+        bufs_.push_back(Buf{p, n, dev, cur});
         bytes_[dev] += n;
         return;
       }
@@ -125,7 +137,7 @@ class ResourceCache {
     for (const Buf& b : bufs_) free_buf(b.p, b.dev);
     bufs_.clear();
     bytes_[0] = bytes_[1] = 0;
-    for (hipStream_t s : streams_) (void) hipStreamDestroy(s);
+    for (const CachedStream& c : streams_) (void) hipStreamDestroy(c.s);
     streams_.clear();
   }
 
@@ -133,7 +145,12 @@ class ResourceCache {
   struct Buf {
     void* p;
     size_t n;
-    bool dev;
+    bool dev;    // device memory (else pinned host)
+    int device;  // current device when it was allocated
+  };
+  struct CachedStream {
+    hipStream_t s;
+    int device;
   };
   static void free_buf(void* p, bool dev) {
     if (dev) (void) hipFree(p);
@@ -142,7 +159,7 @@ class ResourceCache {
   std::mutex mu_;
   std::vector<Buf> bufs_;
   size_t bytes_[2] = {0, 0};
-  std::vector<hipStream_t> streams_;
+  std::vector<CachedStream> streams_;
 };
 
 // Fixed pool of I/O workers; run() executes a batch and waits for it.

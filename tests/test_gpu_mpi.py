@@ -271,3 +271,49 @@ def test_mpi_rank_backends_repeated_calls(oracle, tmp_path, scheme, p, e, lost):
         for path, _ in files[r]:
             assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
         assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[256:256 + e * chunk], want[r]), r
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_mpi_rank_backends_random(oracle, tmp_path, seed):
+    """Seeded random sets through the per-rank backends: scheme, ranks (2-12,
+    within the box's GPU-process limit), encoding, MPI buffer size (odd sizes
+    included), file lists and erasures; parity against the oracle, rebuilt
+    files by CRC32."""
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    rng = np.random.default_rng(9000 + seed)
+    scheme = "xor" if seed % 3 == 2 else "rs"
+    p = int(rng.integers(3 if scheme == "rs" else 2, 13))
+    e = 1 if scheme == "xor" else int(rng.integers(1, min(p - 1, 5) + 1))
+    d = p - e
+    buf = int(rng.choice([4096, 65536, 100_003, 1 << 20]))
+    m = 1 if scheme == "xor" else int(rng.integers(1, e + 1))
+    lost = sorted(rng.choice(p, size=m, replace=False).tolist())
+    tmp = str(tmp_path)
+    files, chunk = _setup(tmp, p, d, rng, int(rng.choice([1000, 150_000, 700_000])))
+    header = [int(rng.integers(0, 5000)) for _ in range(p)]
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, header, reds)
+    crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
+    res = _mpirun(p, [scheme, "encode", e, tmp, buf], timeout=120)
+    assert res.returncode == 0, (scheme, p, e, buf, res.stdout + res.stderr)
+    lofi = [_logical(fl, d * chunk) for fl in files]
+    want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+    if scheme == "rs":
+        oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    else:
+        oracle.xor_encode_set(p, lofi, want, chunk)
+    for r in range(p):
+        assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[header[r]:], want[r]), (scheme, p, e, r)
+    for r in lost:
+        for path, _ in files[r]:
+            os.unlink(path)
+        os.unlink(reds[r])
+    res = _mpirun(p, [scheme, "rebuild", e, tmp, buf] + lost, timeout=120)
+    assert res.returncode == 0, (scheme, p, e, buf, lost, res.stdout + res.stderr)
+    for r in lost:
+        for path, size in files[r]:
+            assert os.path.getsize(path) == size
+            assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
+        blob = np.fromfile(reds[r], dtype=np.uint8)
+        assert np.array_equal(blob[header[r]:header[r] + e * chunk], want[r]), r

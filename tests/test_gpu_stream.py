@@ -296,3 +296,62 @@ def test_config4_full_chunk_stream_windows_and_round_trip(rd, oracle):
         stream.rs_rebuild_stream(codec, lost, C, io, first=c, nstripes=1)
     for key, want in snap.items():
         assert np.array_equal(cells[key], want), key
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_file_stream_random(rd, oracle, tmp_path, seed):
+    """Seeded random file sets through the streaming pipeline: scheme, ranks,
+    encoding, file lists (empty files included), headers, slice size and I/O
+    threads; parity against the oracle, then a rebuild of random members
+    compared by CRC32. Runs back to back in one process, so later cases draw
+    streams and staging slots from the cache earlier ones filled."""
+    redset_amd, stream = rd
+    rng = np.random.default_rng(7000 + seed)
+    scheme = "xor" if seed % 4 == 3 else "rs"
+    p = int(rng.integers(2 if scheme == "xor" else 3, 25))
+    e = 1 if scheme == "xor" else int(rng.integers(1, min(p - 1, 6) + 1))
+    d = p - e
+    tmp = str(tmp_path)
+    maxsize = int(rng.choice([1, 5000, 120_000, 400_000]))
+    files = [_write_member_files(tmp, r, rng, nfiles=int(rng.integers(0, 4)), maxsize=maxsize) for r in range(p)]
+    max_bytes = max([sum(s for _, s in f) for f in files] + [0])
+    chunk = stream.chunk_size_for(max_bytes, d)
+    header = [int(rng.integers(0, 9000)) for _ in range(p)]
+    reds = [os.path.join(tmp, f"rank{r}.{scheme}.redset") for r in range(p)]
+    crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for f in files for path, _ in f}
+    slice_bytes = int(rng.choice([0, 256, 4096, 65536]))
+    threads = int(rng.integers(1, 9))
+    io = stream.FileIO(files, reds, header, chunk)
+    codec = redset_amd.RSCodec(p, e) if scheme == "rs" else None
+    if scheme == "rs":
+        stream.rs_encode_stream(codec, chunk, io, slice_bytes=slice_bytes, io_threads=threads)
+    else:
+        stream.xor_encode_stream(p, chunk, io, slice_bytes=slice_bytes, io_threads=threads)
+    io.close()
+    lofi = [_logical(f, d * chunk) for f in files]
+    want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+    if scheme == "rs":
+        oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    else:
+        oracle.xor_encode_set(p, lofi, want, chunk)
+    for r in range(p):
+        got = np.fromfile(reds[r], dtype=np.uint8)[header[r]:header[r] + e * chunk]
+        assert np.array_equal(got, want[r]), (scheme, p, e, chunk, r)
+    m = 1 if scheme == "xor" else int(rng.integers(1, e + 1))
+    lost = sorted(rng.choice(p, size=m, replace=False).tolist())
+    for r in lost:
+        for path, _ in files[r]:
+            os.unlink(path)
+        os.unlink(reds[r])
+    io = stream.FileIO(files, reds, header, chunk, writable=[r in lost for r in range(p)])
+    if scheme == "rs":
+        stream.rs_rebuild_stream(codec, lost, chunk, io, slice_bytes=slice_bytes, io_threads=threads)
+    else:
+        stream.xor_rebuild_stream(p, lost[0], chunk, io, slice_bytes=slice_bytes, io_threads=threads)
+    io.close()
+    for r in lost:
+        for path, size in files[r]:
+            assert os.path.getsize(path) == size
+            assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
+        got = np.fromfile(reds[r], dtype=np.uint8)[header[r]:header[r] + e * chunk]
+        assert np.array_equal(got, want[r]), (scheme, p, e, chunk, lost, r)

@@ -84,6 +84,13 @@
 #ifndef REDSET_GLDS
 #define REDSET_GLDS 0
 #endif
+// Wave priority (A/B knob, 0 = off): 1 raises s_setprio while a wave issues
+// its loads, 2 while it computes and stores, 3 = 1 for gf_mac with >= 3
+// outputs and for xor, 2 for gf_mac with <= 2 outputs.
+#ifndef REDSET_SETPRIO
+#define REDSET_SETPRIO 0
+#endif
+constexpr int sweep_prio(int nout) { return REDSET_SETPRIO == 3 ? (nout >= 3 ? 1 : 2) : REDSET_SETPRIO; }
 
 #if REDSET_WAVES_PER_EU > 0
 #define REDSET_KERNEL __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(1, REDSET_WAVES_PER_EU)))
@@ -359,7 +366,7 @@ __device__ __forceinline__ void xor_vec(const v4u (&x)[NIN], g_u4* out, size_t v
 // stores zeros to the position its first step will overwrite, so the loop is
 // entered with the same loads-then-stores sequence in flight as on the back
 // edge and the compiler's waits in the first half count the stores too.
-template <int NIN, typename Body, typename Prime>
+template <int NIN, int PRIO, typename Body, typename Prime>
 __device__ __forceinline__ void sweep(g_cu4* const (&in)[NIN], size_t nvec, size_t vstep, int part, Body body,
                                       Prime prime) {
 #if !REDSET_PIPELINE
@@ -367,8 +374,26 @@ __device__ __forceinline__ void sweep(g_cu4* const (&in)[NIN], size_t nvec, size
   (void) prime;
   for (size_t v = static_cast<size_t>(part) * kBlock + threadIdx.x; v < nvec; v += vstep) {
     v4u x[NIN];
-    load_vec<NIN>(x, in, v);
-    body(x, v, true);
+    if constexpr (PRIO == 1) {
+      // a wave issues its loads at raised priority
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(2);
+      load_vec<NIN>(x, in, v);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      load_vec<NIN>(x, in, v);
+    }
+    if constexpr (PRIO == 2) {
+      // the arithmetic and stores run at raised priority
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_setprio(2);
+      body(x, v, true);
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_sched_barrier(0);
+    } else {
+      body(x, v, true);
+    }
   }
   return;
 #endif
@@ -518,7 +543,7 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
     gf_mac_glds_sweep<NIN, NOUT, ACC>(lds, ring, in, out, nvec, vstep,
                                       static_cast<size_t>(part) * kBlock + static_cast<size_t>(wave) * 64);
 #else
-    sweep<NIN>(
+    sweep<NIN, sweep_prio(NOUT)>(
         in, nvec, vstep, part,
         [&](const v4u (&x)[NIN], size_t v, bool st) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, st); },
         [&](size_t v) {
@@ -558,7 +583,7 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
 #pragma unroll
     for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (J.in[i]);
     g_u4* out = (g_u4*) (J.out);
-    sweep<NIN>(
+    sweep<NIN, sweep_prio(3)>(
         in, nvec, vstep, part, [&](const v4u (&x)[NIN], size_t v, bool st) { xor_vec<NIN, ACC>(x, out, v, st); },
         [&](size_t v) {
           if constexpr (!ACC) out[v] = v4u{0, 0, 0, 0};

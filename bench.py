@@ -496,6 +496,9 @@ def main():
     ms_per_step = elapsed * 1e3 / args.steps
     # after the timed region: the round trip on this rank's set, and the box's copy rate
     rt_ok = round_trip(lay, enc_plan, reb_plan, lost, stream)
+    # every launch so far (timed steps included) completed its loader-ring handshakes
+    ring_faults = redset_amd.ring_faults()
+    rt_ok = rt_ok and ring_faults == 0
     if dist_on:
         flag = torch.tensor([int(rt_ok)], dtype=torch.int32, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
@@ -573,6 +576,7 @@ def main():
                           "max": round(max(step_ms), 4)},
     }
     result["round_trip_bit_exact"] = rt_ok
+    result["ring_faults"] = ring_faults
     result["box_reference"] = {
         "torch_copy_GBps": box_copy,
         "codec_vs_copy": round(achieved / box_copy, 4),

@@ -347,6 +347,12 @@ int redset_hip_rccl_transport_create(const unsigned char id[128], int world, int
                                      redset_hip_rccl** handle);
 void redset_hip_rccl_transport_destroy(redset_hip_rccl* handle);
 
+/* Capped handshake spins of the kernels' loader-wave ring on the current
+ * device since the last clearing read (0 in every run so far; nonzero means
+ * some launch produced wrong outputs). Synchronises the device; `clear`
+ * resets the count. */
+int redset_hip_ring_faults(unsigned* count, int clear);
+
 /* Text of the last failure on this thread ("" if none). */
 const char* redset_hip_last_error(void);
 /* For layers built on this library (the per-rank backends of

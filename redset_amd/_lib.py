@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
-from ctypes import POINTER, c_char_p, c_int, c_size_t, c_ubyte, c_ulonglong, c_void_p
+from ctypes import POINTER, c_char_p, c_int, c_size_t, c_ubyte, c_uint, c_ulonglong, c_void_p
 
 # REDSET_HIP_LIBRARY points at another build of the same library (A/B runs)
 LIB_PATH = os.environ.get("REDSET_HIP_LIBRARY") or os.path.join(
@@ -41,6 +41,7 @@ EXPORTED_SYMBOLS = (
     "redset_hip_gf_combine",
     "redset_hip_xor_combine",
     "redset_hip_rs_decode_matrix",
+    "redset_hip_ring_faults",
     "redset_hip_last_error",
     "redset_hip_record_error",
     "redset_hip_version",
@@ -217,6 +218,7 @@ _SIGNATURES = {
     "redset_hip_rccl_unique_id": (c_int, [POINTER(c_ubyte)]),
     "redset_hip_rccl_transport_create": (c_int, [POINTER(c_ubyte), c_int, c_int, POINTER(Transport), POINTER(c_void_p)]),
     "redset_hip_rccl_transport_destroy": (None, [c_void_p]),
+    "redset_hip_ring_faults": (c_int, [POINTER(c_uint), c_int]),
     "redset_hip_last_error": (c_char_p, []),
     "redset_hip_record_error": (c_int, [c_char_p]),
     "redset_hip_version": (c_char_p, []),

@@ -255,3 +255,14 @@ class SetLayout:
 
     def parity_ptrs(self):
         return [self.parity(r).data_ptr() for r in range(self.ranks)]
+
+
+def ring_faults(clear: bool = True) -> int:
+    """Capped loader-ring handshake spins on the current device since the
+    last clearing read (include/redset_hip.h redset_hip_ring_faults; 0 means
+    every launch's ring handshake completed). Synchronises the device."""
+    from ctypes import c_uint
+
+    n = c_uint(0)
+    _lib.check(_lib.load().redset_hip_ring_faults(ctypes.byref(n), int(clear)), "ring_faults")
+    return int(n.value)

@@ -69,12 +69,13 @@
 
 // Register budget of the kernels: N > 0 compiles them for at most N waves
 // per SIMD (amdgpu_waves_per_eu), i.e. up to 512 / N VGPRs; 0 lets the
-// compiler aim for 4 waves (<= 128 VGPRs). The codec runs 8 waves per CU = 2
-// per SIMD (redset_hip.cpp), so 2 costs no occupancy; it lets gf_mac<8,3>
-// issue all 8 input loads of a position before its first wait and measured
-// +1.0% on the RS step (profiles/r01_ab_waves_per_eu.txt).
+// compiler aim for 4 waves (<= 128 VGPRs). The codec runs one block per CU,
+// so the default -- the block's own waves per SIMD (4 for the ring's 1024
+// threads, 2 for the plain sweep's 512) -- costs no occupancy; for the plain
+// sweep it lets gf_mac<8,3> issue all 8 input loads of a position before its
+// first wait (+1.0% on the RS step, profiles/r01_ab_waves_per_eu.txt).
 #ifndef REDSET_WAVES_PER_EU
-#define REDSET_WAVES_PER_EU 2
+#define REDSET_WAVES_PER_EU (REDSET_BLOCK / 256)
 #endif
 // LDS-DMA input ring (A/B knob, 0 = off): every wave streams its inputs
 // with global_load_lds_dwordx4 into a private ring of REDSET_GLDS stages in
@@ -519,6 +520,112 @@ __device__ __forceinline__ void gf_mac_glds_sweep(const uint32_t* tables, l_u4* 
 }
 #endif
 
+#if REDSET_RING
+// Loader-wave LDS-DMA ring (REDSET_RING = D, the items the loader keeps in
+// flight). Wave 0 of the block is the loader: it streams items -- one 1 KiB
+// row (64 lanes x 16 B) of every input -- with global_load_lds_dwordx4 into a
+// ring of S slots in LDS and publishes an item (FULL word of its slot) once
+// a counted vmcnt says it has landed. The other waves (15 at the default
+// 1024 threads) consume items in turn:
+// wait for FULL, ds_read_b128 their lane's 16 B of each input, release the
+// slot (FREE word), combine and store. A consumer never waits on HBM loads or
+// on a store acknowledgement behind them, the loader never on arithmetic.
+// Deadlock freedom: before the loader waits for a free slot it drains and
+// publishes every item it holds, so every issued item is eventually
+// published and consumed. Every spin is bounded (kRingSpinCap polls); a
+// capped spin (never seen) counts in the launch's fault word, which
+// redset_hip_ring_faults() reads, and leaves wrong outputs.
+constexpr int kRingBudget = 128 * 1024;
+template <int NIN>
+constexpr int ring_slots() {
+  return kRingBudget / (NIN * 1024) > 16 ? 16 : kRingBudget / (NIN * 1024);
+}
+constexpr unsigned kRingSpinCap = 1u << 24;
+typedef __attribute__((address_space(3))) v4u lr_u4;
+typedef __attribute__((address_space(3))) volatile unsigned lr_flag;  // LDS, never flat
+__device__ __forceinline__ unsigned ring_flag_ld(unsigned* p) { return *(lr_flag*) p; }
+__device__ __forceinline__ void ring_flag_st(unsigned* p, unsigned v) { *(lr_flag*) p = v; }
+template <int N>
+__device__ __forceinline__ void ring_wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Item k of this block covers vectors (k * G + part) * 64 + lane; `body(x, v)`
+// combines and stores one in-range vector position.
+template <int NIN, typename Body>
+__device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec, size_t G, size_t part,
+                                           unsigned* fault, Body body) {
+  constexpr int S = ring_slots<NIN>(), D = REDSET_RING;
+  static_assert(D >= 1 && D - 1 < S && (D - 1) * NIN <= 63, "ring depth");
+  constexpr int C = kBlock / 64 - 1;
+  static_assert(C >= 1, "a consumer wave");
+  __shared__ v4u ring[S * NIN * 64];
+  __shared__ unsigned full[S], freed[S];
+  if (threadIdx.x < S) full[threadIdx.x] = 0, freed[threadIdx.x] = 0;
+  __syncthreads();
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  const size_t rows = (nvec + 63) / 64;
+  const size_t K = rows > part ? (rows - part + G - 1) / G : 0;
+  if (wave == 0) {
+    const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lr_u4*) ring)));
+    // items [pub, k) are issued and not yet published
+    size_t pub = 0;
+    auto publish = [&]() {
+      if (lane == 0) ring_flag_st(&full[pub % S], static_cast<unsigned>(pub / S) + 1);
+      ++pub;
+    };
+    for (size_t k = 0; k < K; ++k) {
+      const unsigned use = static_cast<unsigned>(k / S);
+      if (ring_flag_ld(&freed[k % S]) < use) {
+        ring_wait_vm<0>();
+        while (pub < k) publish();
+        unsigned spins = 0;
+        while (ring_flag_ld(&freed[k % S]) < use && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+        if (spins >= kRingSpinCap && lane == 0 && fault) atomicAdd(fault, 1u);
+      }
+      const size_t v = (k * G + part) * 64 + lane;
+      const size_t vc = v < nvec ? v : nvec - 1;
+      const uint32_t slot = ring0 + static_cast<uint32_t>((k % S) * NIN * 1024);
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) {
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+#if REDSET_LOAD_POLICY == 1
+            " nt"
+#endif
+            "\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"(in[i] + vc), "s"(slot + static_cast<uint32_t>(i * 1024))
+            : "memory");
+      }
+      if (k + 1 - pub == static_cast<size_t>(D)) {
+        ring_wait_vm<(D - 1) * NIN>();  // the oldest pending item has landed
+        publish();
+      }
+    }
+    ring_wait_vm<0>();
+    while (pub < K) publish();
+    return;
+  }
+  for (size_t k = wave - 1; k < K; k += C) {
+    const unsigned want = static_cast<unsigned>(k / S) + 1;
+    unsigned spins = 0;
+    while (ring_flag_ld(&full[k % S]) < want && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+    if (spins >= kRingSpinCap && lane == 0 && fault) atomicAdd(fault, 1u);
+    const lr_u4* sl = (const lr_u4*) ring + (k % S) * NIN * 64;
+    v4u x[NIN];
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) x[i] = sl[i * 64 + lane];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if (lane == 0) ring_flag_st(&freed[k % S], want);
+    const size_t v = (k * G + part) * 64 + lane;
+    if (v < nvec) body(x, v);
+  }
+}
+#endif
+
 template <int NIN, int NOUT, bool ACC>
 __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, int part) {
   // static (not extern) so the table offsets fold into ds_read's immediate
@@ -536,7 +643,10 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
     g_u4* out[NOUT];
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) out[j] = (g_u4*) (J.out[j]);
-#if REDSET_GLDS
+#if REDSET_RING
+    ring_sweep<NIN>(in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
+                    [&](const v4u (&x)[NIN], size_t v) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, true); });
+#elif REDSET_GLDS
     __shared__ v4u ring_mem[glds_stages<NIN>() * NIN * 64 * kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
     l_u4* ring = (l_u4*) (ring_mem) + wave * glds_stages<NIN>() * NIN * 64;
@@ -583,11 +693,16 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
 #pragma unroll
     for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (J.in[i]);
     g_u4* out = (g_u4*) (J.out);
+#if REDSET_RING
+    ring_sweep<NIN>(in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
+                    [&](const v4u (&x)[NIN], size_t v) { xor_vec<NIN, ACC>(x, out, v, true); });
+#else
     sweep<NIN, sweep_prio(3)>(
         in, nvec, vstep, part, [&](const v4u (&x)[NIN], size_t v, bool st) { xor_vec<NIN, ACC>(x, out, v, st); },
         [&](size_t v) {
           if constexpr (!ACC) out[v] = v4u{0, 0, 0, 0};
         });
+#endif
   }
   const size_t tail0 = nvec * 16;
   for (size_t k = tail0 + static_cast<size_t>(part) * kBlock + threadIdx.x; k < L.nbytes; k += vstep) {

@@ -43,6 +43,7 @@ struct GfLaunch {
   int job0;                 // first job of this launch (set by the launcher)
   int group;                // kJobsInLaunches: jobs per launch, side by side (0 = 1)
   size_t nbytes;            // bytes per cell
+  unsigned* fault;          // set by the launcher: counts capped ring spins (codec_device.h)
 };
 
 // XOR of `nin` inputs into one output (the XOR scheme's parity / rebuild).
@@ -62,6 +63,7 @@ struct XorLaunch {
   int job0;
   int group;
   size_t nbytes;
+  unsigned* fault;          // set by the launcher (see GfLaunch)
 };
 
 // launchers (codec_kernels.hip); return hipError_t as int
@@ -72,13 +74,29 @@ int launch_gf_single(const GfLaunch& L, const GfJob& J, void* stream);
 int launch_xor_single(const XorLaunch& L, const XorJob& J, void* stream);
 // device properties used to size grids
 int device_cu_count();
+// the current device's count of capped loader-ring spins since the last
+// read (a ring handshake that never completed; its outputs are wrong);
+// `clear` resets it. Synchronises the device. Returns hipError_t as int.
+int read_ring_faults(unsigned* count, int clear);
 // occupancy of the GF kernel for a given input count (blocks per CU)
 int gf_blocks_per_cu(int nin);
 
+// Sweep of the kernels (codec_device.h): REDSET_RING = D > 0 streams the
+// inputs through a loader-wave LDS-DMA ring with D items in flight
+// (ring_sweep), 0 = the plain per-wave sweep.
+#ifndef REDSET_RING
+#define REDSET_RING 3
+#endif
+// Threads per block, one block per CU: the ring runs 1 loader + 15 consumer
+// waves (1024), the plain sweep 8 waves (512). A/B in profiles/r02_ab_ring.txt,
+// r02_ab_block_waves.txt.
 #ifndef REDSET_BLOCK
+#if REDSET_RING
+#define REDSET_BLOCK 1024
+#else
 #define REDSET_BLOCK 512
 #endif
-// threads per block (A/B knob: 512 = one block per CU at the same waves per CU)
+#endif
 constexpr int kBlock = REDSET_BLOCK;
 
 // The kernels of one input count: [nout - 1][accumulate] for gf_mac,

@@ -36,7 +36,32 @@ int jobs_per_launch(const Launch& L) {
   return L.sequential == kJobsInLaunches ? std::max(1, L.group) : L.njobs;
 }
 
+// Capped loader-ring spins (codec_device.h ring_sweep), one word per device:
+// the kernels get its address in GfLaunch / XorLaunch::fault.
+__device__ unsigned g_ring_fault;
+
+unsigned* ring_fault_word() {
+  static unsigned* addr[64] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  if (!addr[dev]) {
+    void* p = nullptr;
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_ring_fault)) == hipSuccess) addr[dev] = static_cast<unsigned*>(p);
+  }
+  return addr[dev];
+}
 }  // namespace
+
+int read_ring_faults(unsigned* count, int clear) {
+  unsigned v = 0;
+  hipError_t e = hipMemcpyFromSymbol(&v, HIP_SYMBOL(g_ring_fault), sizeof(v), 0, hipMemcpyDeviceToHost);
+  if (e == hipSuccess && clear && v) {
+    const unsigned zero = 0;
+    e = hipMemcpyToSymbol(HIP_SYMBOL(g_ring_fault), &zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+  }
+  if (count) *count = v;
+  return e;
+}
 
 int device_cu_count() {
   static int cus = 0;
@@ -75,6 +100,7 @@ int launch_gf(const GfLaunch& L, void* stream) {
   for (int j = 0; j < L.njobs; j += per) {
     GfLaunch one = L;
     one.job0 = j;
+    one.fault = ring_fault_word();
     const int n = L.sequential == kJobsInKernel ? 1 : std::min(per, L.njobs - j);
     const dim3 grid(static_cast<unsigned>(n * L.blocks_per_job));
     hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), one);
@@ -87,16 +113,20 @@ int launch_gf(const GfLaunch& L, void* stream) {
 int launch_gf_single(const GfLaunch& L, const GfJob& J, void* stream) {
   if (L.nin < 1 || L.nin > kMaxIn || L.nout < 1 || L.nout > kMaxOut) return hipErrorInvalidValue;
   if (L.nbytes == 0) return hipSuccess;
+  GfLaunch one = L;
+  one.fault = ring_fault_word();
   hipLaunchKernelGGL(kernel_set(L.nin).gf_arg[L.nout - 1][L.accumulate ? 1 : 0], dim3(static_cast<unsigned>(L.blocks_per_job)), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), L, J);
+                     static_cast<hipStream_t>(stream), one, J);
   return hipGetLastError();
 }
 
 int launch_xor_single(const XorLaunch& L, const XorJob& J, void* stream) {
   if (L.nin < 1 || L.nin > kMaxIn) return hipErrorInvalidValue;
   if (L.nbytes == 0) return hipSuccess;
+  XorLaunch one = L;
+  one.fault = ring_fault_word();
   hipLaunchKernelGGL(kernel_set(L.nin).xr_arg[L.accumulate ? 1 : 0], dim3(static_cast<unsigned>(L.blocks_per_job)), dim3(kBlock), 0,
-                     static_cast<hipStream_t>(stream), L, J);
+                     static_cast<hipStream_t>(stream), one, J);
   return hipGetLastError();
 }
 
@@ -108,6 +138,7 @@ int launch_xor(const XorLaunch& L, void* stream) {
   for (int j = 0; j < L.njobs; j += per) {
     XorLaunch one = L;
     one.job0 = j;
+    one.fault = ring_fault_word();
     const int n = L.sequential == kJobsInKernel ? 1 : std::min(per, L.njobs - j);
     const dim3 grid(static_cast<unsigned>(n * L.blocks_per_job));
     hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), one);

@@ -358,6 +358,10 @@ int run_stripe(const StripeMap& m, const uint8_t* const* in, uint8_t* const* out
 
 extern "C" {
 
+int redset_hip_ring_faults(unsigned* count, int clear) {
+  if (!count) return fail("ring_faults: null argument");
+  return hip_check(static_cast<hipError_t>(redset_hip::read_ring_faults(count, clear)), "ring_faults");
+}
 const char* redset_hip_last_error(void) { return redset_hip::last_error(); }
 int redset_hip_record_error(const char* msg) { return fail("%s", msg ? msg : "unknown error"); }
 

@@ -31,3 +31,20 @@ def oracle():
 
     oracle_lib.build()
     return oracle_lib
+
+
+@pytest.fixture(autouse=True)
+def _no_ring_faults(request):
+    """After every GPU test that used the codec in this process: no kernel's
+    loader-ring handshake hit its spin cap (codec_device.h ring_sweep; a
+    capped spin means wrong outputs, so it fails the test loudly)."""
+    yield
+    if request.node.get_closest_marker("gpu") is None:
+        return
+    import redset_amd._lib as L
+
+    if L._lib is None or not gpu_available():
+        return
+    import redset_amd
+
+    assert redset_amd.ring_faults() == 0, "a loader-ring handshake hit its spin cap"

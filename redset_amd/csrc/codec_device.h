@@ -535,10 +535,21 @@ __device__ __forceinline__ void gf_mac_glds_sweep(const uint32_t* tables, l_u4* 
 // published and consumed. Every spin is bounded (kRingSpinCap polls); a
 // capped spin (never seen) counts in the launch's fault word, which
 // redset_hip_ring_faults() reads, and leaves wrong outputs.
-constexpr int kRingBudget = 128 * 1024;
+#ifndef REDSET_RING_KIB
+#define REDSET_RING_KIB 128
+#endif
+// 1: a loader that finds its next slot busy first drains and publishes
+// what it holds (A/B knob; 0 = spin on the slot with its items pending)
+#ifndef REDSET_RING_DRAIN
+#define REDSET_RING_DRAIN 1
+#endif
+constexpr int kRingBudget = REDSET_RING_KIB * 1024;
+#ifndef REDSET_RING_MAX_SLOTS
+#define REDSET_RING_MAX_SLOTS 16
+#endif
 template <int NIN>
 constexpr int ring_slots() {
-  return kRingBudget / (NIN * 1024) > 16 ? 16 : kRingBudget / (NIN * 1024);
+  return kRingBudget / (NIN * 1024) > REDSET_RING_MAX_SLOTS ? REDSET_RING_MAX_SLOTS : kRingBudget / (NIN * 1024);
 }
 constexpr unsigned kRingSpinCap = 1u << 24;
 typedef __attribute__((address_space(3))) v4u lr_u4;
@@ -578,8 +589,10 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
     for (size_t k = 0; k < K; ++k) {
       const unsigned use = static_cast<unsigned>(k / S);
       if (ring_flag_ld(&freed[k % S]) < use) {
+#if REDSET_RING_DRAIN
         ring_wait_vm<0>();
         while (pub < k) publish();
+#endif
         unsigned spins = 0;
         while (ring_flag_ld(&freed[k % S]) < use && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
         if (spins >= kRingSpinCap && lane == 0 && fault) atomicAdd(fault, 1u);

@@ -53,12 +53,13 @@ int hip_check(hipError_t e, const char* what) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// Resident blocks per CU the codec aims for: 8 waves per CU (2 blocks of 256
-// threads or 1 of 512). HBM streams best at low occupancy here: 8 waves
-// (64 KiB of loads in flight) per CU beat 4, 12, 16 and 32 on every box
-// measured (tools/bpc_sweep.sh, profiles/r01_ab_pipeline.txt,
-// r01_ab_waves_per_eu.txt; 4 waves leave the lookups uncovered, more add DRAM
-// row contention); REDSET_HIP_BLOCKS_PER_CU overrides it.
+// Resident blocks per CU the codec aims for: one block (the ring's 1024
+// threads = 1 loader + 15 consumer waves, or the plain sweep's 512 = 8
+// waves; codec_kernels.h). For the plain sweep 8 waves (64 KiB of loads in
+// flight) per CU beat 4, 12, 16 and 32 on every box measured
+// (tools/bpc_sweep.sh, profiles/r01_ab_pipeline.txt, r01_ab_waves_per_eu.txt);
+// the ring needs its block alone on the CU (128 KiB of LDS).
+// REDSET_HIP_BLOCKS_PER_CU overrides it.
 int target_blocks_per_cu(int occupancy) {
   static int env = -1;
   if (env < 0) {
@@ -69,11 +70,11 @@ int target_blocks_per_cu(int occupancy) {
   return std::max(1, std::min(want, occupancy));
 }
 
-// Resident XOR blocks per CU. The XOR kernel has no tables and little VALU
-// work: with 256-thread blocks one block per CU (4 waves) ran its 7 read
-// streams at 6.00 TB/s against 5.78 at two (profiles/r01_ab_xor_blocks.txt);
-// with 512-thread blocks one block (8 waves) runs 5.98-6.00
-// (profiles/r01_ab_block_size.txt). REDSET_HIP_XOR_BLOCKS_PER_CU overrides it.
+// Resident XOR blocks per CU: one. With the plain sweep, 256-thread blocks
+// one per CU (4 waves) ran the 7 read streams at 6.00 TB/s against 5.78 at
+// two (profiles/r01_ab_xor_blocks.txt) and 512-thread blocks (8 waves)
+// 5.98-6.00 (profiles/r01_ab_block_size.txt); the ring's block fills the
+// CU's LDS. REDSET_HIP_XOR_BLOCKS_PER_CU overrides it.
 int xor_blocks_cap() {
   static int env = -1;
   if (env < 0) {

@@ -521,9 +521,9 @@ __device__ __forceinline__ void gf_mac_glds_sweep(const uint32_t* tables, l_u4* 
 #endif
 
 #if REDSET_RING
-// Loader-wave LDS-DMA ring (REDSET_RING = D, the items the loader keeps in
-// flight). Wave 0 of the block is the loader: it streams items -- one 1 KiB
-// row (64 lanes x 16 B) of every input -- with global_load_lds_dwordx4 into a
+// Loader-wave LDS-DMA ring (shape per kernel below: D items in flight, R
+// rows per item). Wave 0 of the block is the loader: it streams items -- R
+// 1 KiB rows (64 lanes x 16 B) of every input -- with global_load_lds_dwordx4 into a
 // ring of S slots in LDS and publishes an item (FULL word of its slot) once
 // a counted vmcnt says it has landed. The other waves (15 at the default
 // 1024 threads) consume items in turn:
@@ -544,6 +544,19 @@ __device__ __forceinline__ void gf_mac_glds_sweep(const uint32_t* tables, l_u4* 
 #define REDSET_RING_DRAIN 1
 #endif
 constexpr int kRingBudget = REDSET_RING_KIB * 1024;
+// Ring shape per kernel: R = 64-vector rows of every input per item, D =
+// items the loader keeps in flight. gf_mac: 1 row, D = REDSET_RING (the
+// consumers' GF math sets part of the pace; two-row items cost 3%). XOR: 2
+// rows, D = 2 (+3-4% over 1 row, D = 3; profiles/r02_ab_ring_rows.txt).
+#ifndef REDSET_RING_GF_ROWS
+#define REDSET_RING_GF_ROWS 1
+#endif
+#ifndef REDSET_RING_XOR_ROWS
+#define REDSET_RING_XOR_ROWS 2
+#endif
+#ifndef REDSET_RING_XOR_DEPTH
+#define REDSET_RING_XOR_DEPTH 2
+#endif
 #ifndef REDSET_RING_MAX_SLOTS
 #define REDSET_RING_MAX_SLOTS 16
 #endif
@@ -563,21 +576,24 @@ __device__ __forceinline__ void ring_wait_vm() {
 
 // Item k of this block covers vectors (k * G + part) * 64 + lane; `body(x, v)`
 // combines and stores one in-range vector position.
-template <int NIN, typename Body>
+template <int NIN, int R, int D, typename Body>
 __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec, size_t G, size_t part,
                                            unsigned* fault, Body body) {
-  constexpr int S = ring_slots<NIN>(), D = REDSET_RING;
-  static_assert(D >= 1 && D - 1 < S && (D - 1) * NIN <= 63, "ring depth");
+  constexpr int S = ring_slots<NIN * R>();
+  static_assert(D >= 1 && D - 1 < S && (D - 1) * NIN * R <= 63, "ring depth");
   constexpr int C = kBlock / 64 - 1;
   static_assert(C >= 1, "a consumer wave");
-  __shared__ v4u ring[S * NIN * 64];
+  __shared__ v4u ring[S * NIN * R * 64];
   __shared__ unsigned full[S], freed[S];
   if (threadIdx.x < S) full[threadIdx.x] = 0, freed[threadIdx.x] = 0;
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   const size_t rows = (nvec + 63) / 64;
-  const size_t K = rows > part ? (rows - part + G - 1) / G : 0;
+  const size_t items = (rows + R - 1) / R;
+  const size_t K = items > part ? (items - part + G - 1) / G : 0;
+  // vector of row r of item k in this block
+  auto vec_of = [&](size_t k, int r) { return ((k * G + part) * R + r) * 64 + lane; };
   if (wave == 0) {
     const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lr_u4*) ring)));
     // items [pub, k) are issued and not yet published
@@ -597,24 +613,27 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
         while (ring_flag_ld(&freed[k % S]) < use && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
         if (spins >= kRingSpinCap && lane == 0 && fault) atomicAdd(fault, 1u);
       }
-      const size_t v = (k * G + part) * 64 + lane;
-      const size_t vc = v < nvec ? v : nvec - 1;
-      const uint32_t slot = ring0 + static_cast<uint32_t>((k % S) * NIN * 1024);
+      const uint32_t slot = ring0 + static_cast<uint32_t>((k % S) * NIN * R * 1024);
 #pragma unroll
-      for (int i = 0; i < NIN; ++i) {
-        uint32_t keep;
-        asm volatile(
-            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+      for (int r = 0; r < R; ++r) {
+        const size_t v = vec_of(k, r);
+        const size_t vc = v < nvec ? v : nvec - 1;
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) {
+          uint32_t keep;
+          asm volatile(
+              "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
 #if REDSET_LOAD_POLICY == 1
-            " nt"
+              " nt"
 #endif
-            "\n\ts_mov_b32 m0, %0"
-            : "=&s"(keep)
-            : "v"(in[i] + vc), "s"(slot + static_cast<uint32_t>(i * 1024))
-            : "memory");
+              "\n\ts_mov_b32 m0, %0"
+              : "=&s"(keep)
+              : "v"(in[i] + vc), "s"(slot + static_cast<uint32_t>((i * R + r) * 1024))
+              : "memory");
+        }
       }
       if (k + 1 - pub == static_cast<size_t>(D)) {
-        ring_wait_vm<(D - 1) * NIN>();  // the oldest pending item has landed
+        ring_wait_vm<(D - 1) * NIN * R>();  // the oldest pending item has landed
         publish();
       }
     }
@@ -627,14 +646,19 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
     unsigned spins = 0;
     while (ring_flag_ld(&full[k % S]) < want && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
     if (spins >= kRingSpinCap && lane == 0 && fault) atomicAdd(fault, 1u);
-    const lr_u4* sl = (const lr_u4*) ring + (k % S) * NIN * 64;
-    v4u x[NIN];
+    const lr_u4* sl = (const lr_u4*) ring + (k % S) * NIN * R * 64;
+    v4u x[R][NIN];
 #pragma unroll
-    for (int i = 0; i < NIN; ++i) x[i] = sl[i * 64 + lane];
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) x[r][i] = sl[(i * R + r) * 64 + lane];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     if (lane == 0) ring_flag_st(&freed[k % S], want);
-    const size_t v = (k * G + part) * 64 + lane;
-    if (v < nvec) body(x, v);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const size_t v = vec_of(k, r);
+      if (v < nvec) body(x[r], v);
+    }
   }
 }
 #endif
@@ -657,8 +681,9 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) out[j] = (g_u4*) (J.out[j]);
 #if REDSET_RING
-    ring_sweep<NIN>(in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
-                    [&](const v4u (&x)[NIN], size_t v) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, true); });
+    ring_sweep<NIN, REDSET_RING_GF_ROWS, REDSET_RING>(
+        in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
+        [&](const v4u (&x)[NIN], size_t v) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, true); });
 #elif REDSET_GLDS
     __shared__ v4u ring_mem[glds_stages<NIN>() * NIN * 64 * kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
@@ -707,8 +732,9 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
     for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (J.in[i]);
     g_u4* out = (g_u4*) (J.out);
 #if REDSET_RING
-    ring_sweep<NIN>(in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
-                    [&](const v4u (&x)[NIN], size_t v) { xor_vec<NIN, ACC>(x, out, v, true); });
+    ring_sweep<NIN, REDSET_RING_XOR_ROWS, REDSET_RING_XOR_DEPTH>(
+        in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
+        [&](const v4u (&x)[NIN], size_t v) { xor_vec<NIN, ACC>(x, out, v, true); });
 #else
     sweep<NIN, sweep_prio(3)>(
         in, nvec, vstep, part, [&](const v4u (&x)[NIN], size_t v, bool st) { xor_vec<NIN, ACC>(x, out, v, st); },

@@ -557,6 +557,11 @@ constexpr int kRingBudget = REDSET_RING_KIB * 1024;
 #ifndef REDSET_RING_XOR_DEPTH
 #define REDSET_RING_XOR_DEPTH 2
 #endif
+// s_sleep argument (x 64 clocks) between a consumer's polls of a FULL word:
+// polls take issue slots from the co-resident consumers that are computing
+#ifndef REDSET_RING_SLEEP
+#define REDSET_RING_SLEEP 1
+#endif
 #ifndef REDSET_RING_MAX_SLOTS
 #define REDSET_RING_MAX_SLOTS 16
 #endif
@@ -644,7 +649,7 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
   for (size_t k = wave - 1; k < K; k += C) {
     const unsigned want = static_cast<unsigned>(k / S) + 1;
     unsigned spins = 0;
-    while (ring_flag_ld(&full[k % S]) < want && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+    while (ring_flag_ld(&full[k % S]) < want && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(REDSET_RING_SLEEP);
     if (spins >= kRingSpinCap && lane == 0 && fault) atomicAdd(fault, 1u);
     const lr_u4* sl = (const lr_u4*) ring + (k % S) * NIN * R * 64;
     v4u x[R][NIN];

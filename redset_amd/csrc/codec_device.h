@@ -559,8 +559,11 @@ constexpr int kRingBudget = REDSET_RING_KIB * 1024;
 #endif
 // s_sleep argument (x 64 clocks) between a consumer's polls of a FULL word:
 // polls take issue slots from the co-resident consumers that are computing
+// (~17% of the LDS instructions at 1, profiles/r02s60_ring_pmc_lds.txt);
+// 8 measured +0.9% on the RS step, rebuild +1.5-2% (4 and 16 alike;
+// profiles/r02_ab_ring_sleep.txt)
 #ifndef REDSET_RING_SLEEP
-#define REDSET_RING_SLEEP 1
+#define REDSET_RING_SLEEP 8
 #endif
 #ifndef REDSET_RING_MAX_SLOTS
 #define REDSET_RING_MAX_SLOTS 16

@@ -593,6 +593,10 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
   static_assert(C >= 1, "a consumer wave");
   __shared__ v4u ring[S * NIN * R * 64];
   __shared__ unsigned full[S], freed[S];
+  // every wave has left the ring's previous use (a kernel looping over jobs
+  // calls this once per job: the loader finishes a job first and must not
+  // reset flags that consumers of that job still poll)
+  __syncthreads();
   if (threadIdx.x < S) full[threadIdx.x] = 0, freed[threadIdx.x] = 0;
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);

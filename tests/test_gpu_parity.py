@@ -294,6 +294,37 @@ def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     assert all(np.array_equal(a, b) for a, b in zip(xgot, xc))
 
 
+@pytest.mark.parametrize("mode", ["2", "0", "1"])
+def test_ring_jobs_back_to_back(rd, oracle, monkeypatch, mode):
+    """The kernels' loader-wave ring is reused job after job inside one launch
+    (REDSET_HIP_SEQUENTIAL=2: every block loops over the stripes) and launch
+    after launch: repeated RS and XOR plans over small and ragged cells must
+    stay bit-exact with no capped handshake poll (a loader that reset the next
+    job's flags while consumers still polled the last one's hit the cap in
+    round 2, profiles/r02s62_gpu_tests_ring_fault.log)."""
+    monkeypatch.setenv("REDSET_HIP_SEQUENTIAL", mode)
+    for chunk in (1_000, 65_536 + 48, 300_016):
+        p, e = 11, 3
+        lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=chunk)
+        lay = upload_set(rd, lofi, parity, p - e, e, chunk)
+        codec = rd.RSCodec(p, e)
+        enc = codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+        xl, xc = oracle.random_set(8, 7, 1, chunk, seed=chunk + 1)
+        xlay = upload_set(rd, xl, xc, 7, 1, chunk)
+        xenc = rd.xor_plan_encode(8, xlay.lofi_ptrs(), xlay.parity_ptrs(), chunk, xlay.cell_stride)
+        for _ in range(20):
+            enc.execute()
+            xenc.execute()
+        torch.cuda.synchronize()
+        assert rd.ring_faults() == 0
+        oracle.OracleRS(p, e).encode_set(lofi, parity, chunk)
+        oracle.xor_encode_set(8, xl, xc, chunk)
+        _, got = download_set(lay)
+        _, xgot = download_set(xlay)
+        assert all(np.array_equal(a, b) for a, b in zip(got, parity))
+        assert all(np.array_equal(a, b) for a, b in zip(xgot, xc))
+
+
 def test_zero_length_calls_are_noops(rd):
     """Zero-byte stripe primitives and zero-chunk plans succeed without
     touching their outputs (redset never makes a chunk smaller than 1 byte,

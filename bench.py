@@ -32,6 +32,8 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
+# xGMI: per link and direction (7 links x ~153 GB/s per GPU)
+XGMI_LINK_GBPS = 153.0
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MIB = 1 << 20
 
@@ -385,21 +387,56 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
                       device="cuda" if dist.get_backend() == "nccl" else "cpu")
     dist.all_reduce(ok, op=dist.ReduceOp.MIN)
     value = world * runner.algorithmic_bytes("rebuild") / s_step / 1e9
+    # bytes each GPU sends over the fabric per rebuild (C planner's count),
+    # mean and max over the ranks
+    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
+    sent = torch.tensor([float(runner.exchanged_bytes("rebuild"))], dtype=torch.float64, device=dev)
+    sent_max = sent.clone()
+    dist.all_reduce(sent, op=dist.ReduceOp.SUM)
+    dist.all_reduce(sent_max, op=dist.ReduceOp.MAX)
+    sent_mean, sent_max = sent.item() / world, sent_max.item()
     # untimed diagnostic: the same rebuild with its three phases one after
     # another (no overlap across sets), timed apart by events on rank 0
     pipelined_event_ms = runner.phase_ms().get("rebuild_start->done")
     runner.phased = True
     timed(lambda i: runner.rebuild(), 3, 1, True, before=runner.reset_timing)
+    phases = runner.phase_ms()
+    compute_ms = phases.get("rebuild_gathered->computed")
+    # The step's roofline is the fabric, not HBM: every GPU sends its
+    # share of the decode inputs' slices to every other GPU and gets the
+    # rebuilt slices back (an all-to-all over the node's fully connected
+    # xGMI mesh: one link per peer pair, world - 1 links usable per GPU).
+    link_peak = (world - 1) * XGMI_LINK_GBPS
+    fabric_gbps = sent_mean / s_step / 1e9
     out = {
         "workload": (f"{world} sets of p={p} (RS({p - e}+{e}), chunk {chunk >> 20} MiB), members round-robin over "
                      f"{world} GPUs; rebuild of members {lost} of every set, column-sharded (BASELINE.json configs[3])"),
         "value": round(value, 2),
         "unit": "GB/s",
-        "frac": round(value / world / HBM_PEAK_GBPS, 4),
         "ms_per_step": round(s_step * 1e3, 4),
         "bit_exact": bool(ok.item()),
         "schedule": "sets pipelined: set k+1's gather overlaps set k's gf_mac (redset_hip_sharded_execute)",
         "pipelined_event_ms_rank0": pipelined_event_ms,
+        "roofline": {
+            "bound": "xgmi",
+            "achieved": round(fabric_gbps, 2) if world > 1 else None,
+            "peak": link_peak if world > 1 else None,
+            "unit": "GB/s per GPU (bytes sent over the fabric / step time)",
+            "frac": round(fabric_gbps / link_peak, 4) if world > 1 else None,
+            "bytes_sent_per_gpu_per_step": {"mean": int(sent_mean), "max": int(sent_max)},
+            "peak_source": (f"{XGMI_LINK_GBPS:g} GB/s per xGMI link and direction x (world - 1) links: one link per "
+                            "GPU pair of the node's fully connected mesh, 7 per GPU at 8 GPUs (SURVEY.md §5; "
+                            "MI355X platform figure, not measured here)"),
+        },
+        # HBM is the bound of the compute phase alone (phased diagnostic)
+        "compute_hbm": {
+            "phase_ms_rank0": compute_ms,
+            "achieved": (round(runner.algorithmic_bytes("rebuild") / (compute_ms * 1e-3) / 1e9, 1)
+                         if compute_ms else None),
+            "peak": HBM_PEAK_GBPS,
+            "frac": (round(runner.algorithmic_bytes("rebuild") / (compute_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+                     if compute_ms else None),
+        },
     }
     out.update(runner.report(s_step, "rebuild"))
     return out

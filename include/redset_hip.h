@@ -348,9 +348,15 @@ int redset_hip_rccl_transport_create(const unsigned char id[128], int world, int
 void redset_hip_rccl_transport_destroy(redset_hip_rccl* handle);
 
 /* Capped handshake spins of the kernels' loader-wave ring on the current
- * device since the last clearing read (0 in every run so far; nonzero means
- * some launch produced wrong outputs). Synchronises the device; `clear`
- * resets the count. */
+ * device since the last clearing read. A capped spin never costs
+ * correctness: the waiting consumer (or, after a capped loader, every
+ * consumer of the rest of the launch) loads its bytes straight from HBM, so
+ * every call's outputs are right whatever this returns. A nonzero count in
+ * the shipped build (cap 2^24 polls) means a ring stalled and ran slower --
+ * a performance event worth reporting, not an error. It happened once in
+ * development, from a since-fixed missing barrier (round 2). The count is
+ * per device and process-wide, so concurrent callers share it.
+ * Synchronises the device; `clear` resets the count. */
 int redset_hip_ring_faults(unsigned* count, int clear);
 
 /* Text of the last failure on this thread ("" if none). */

@@ -259,8 +259,10 @@ class SetLayout:
 
 def ring_faults(clear: bool = True) -> int:
     """Capped loader-ring handshake spins on the current device since the
-    last clearing read (include/redset_hip.h redset_hip_ring_faults; 0 means
-    every launch's ring handshake completed). Synchronises the device."""
+    last clearing read (include/redset_hip.h redset_hip_ring_faults). Outputs
+    are correct either way -- a capped spin falls back to direct HBM loads --
+    so this is a stall counter: 0 means every launch's ring handshake
+    completed in time. Synchronises the device."""
     from ctypes import c_uint
 
     n = c_uint(0)

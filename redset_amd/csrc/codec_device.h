@@ -532,9 +532,20 @@ __device__ __forceinline__ void gf_mac_glds_sweep(const uint32_t* tables, l_u4* 
 // on a store acknowledgement behind them, the loader never on arithmetic.
 // Deadlock freedom: before the loader waits for a free slot it drains and
 // publishes every item it holds, so every issued item is eventually
-// published and consumed. Every spin is bounded (kRingSpinCap polls); a
-// capped spin (never seen) counts in the launch's fault word, which
-// redset_hip_ring_faults() reads, and leaves wrong outputs.
+// published and consumed.
+//
+// The ring is only staging: every spin is bounded (kRingSpinCap polls) and
+// a capped spin never costs correctness. A consumer whose FULL wait caps
+// loads its lane's 16 B of each input straight from HBM (and releases the
+// slot); a loader whose FREE wait caps stops streaming without touching the
+// busy slot and raises the block's BYPASS word, after which every item it
+// has not published is loaded directly by its consumer. Each capped spin
+// adds 1 to the launch's fault word (redset_hip_ring_faults()): a
+// performance event, not an error. Capped spins did happen once, from a
+// missing barrier between the jobs of an in-kernel job loop (round 2,
+// profiles/r02s62_gpu_tests_ring_fault.log, fixed at the top of ring_sweep);
+// a build with -DREDSET_RING_SPIN_CAP=4 drives both fallbacks on every
+// launch and is checked bit for bit (tests/test_gpu_ring_fallback.py).
 #ifndef REDSET_RING_KIB
 #define REDSET_RING_KIB 128
 #endif
@@ -557,6 +568,10 @@ constexpr int kRingBudget = REDSET_RING_KIB * 1024;
 #ifndef REDSET_RING_XOR_DEPTH
 #define REDSET_RING_XOR_DEPTH 2
 #endif
+// XOR kernels with more inputs than this use the one-row GF shape (A/B knob)
+#ifndef REDSET_RING_XOR_WIDE
+#define REDSET_RING_XOR_WIDE 8
+#endif
 // s_sleep argument (x 64 clocks) between a consumer's polls of a FULL word:
 // polls take issue slots from the co-resident consumers that are computing
 // (~17% of the LDS instructions at 1, profiles/r02s60_ring_pmc_lds.txt);
@@ -572,7 +587,12 @@ template <int NIN>
 constexpr int ring_slots() {
   return kRingBudget / (NIN * 1024) > REDSET_RING_MAX_SLOTS ? REDSET_RING_MAX_SLOTS : kRingBudget / (NIN * 1024);
 }
-constexpr unsigned kRingSpinCap = 1u << 24;
+// polls before a handshake gives up on the ring (A/B and test knob: a
+// tiny cap exercises the direct-load fallbacks on every launch)
+#ifndef REDSET_RING_SPIN_CAP
+#define REDSET_RING_SPIN_CAP (1u << 24)
+#endif
+constexpr unsigned kRingSpinCap = REDSET_RING_SPIN_CAP;
 typedef __attribute__((address_space(3))) v4u lr_u4;
 typedef __attribute__((address_space(3))) volatile unsigned lr_flag;  // LDS, never flat
 __device__ __forceinline__ unsigned ring_flag_ld(unsigned* p) { return *(lr_flag*) p; }
@@ -580,6 +600,17 @@ __device__ __forceinline__ void ring_flag_st(unsigned* p, unsigned v) { *(lr_fla
 template <int N>
 __device__ __forceinline__ void ring_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+// A consumer's fallback load of one input vector, complete on return: the
+// load and its wait are one asm block, so the compiler never sees a VMEM
+// load pending into the registers the ring path fills with ds_read (it would
+// otherwise put an s_waitcnt vmcnt(0) -- a wait for this consumer's stores --
+// in front of every ring read). The wait drains the wave's stores too, which
+// only the rare fallback pays.
+__device__ __forceinline__ v4u ring_direct_load(g_cu4* p) {
+  v4u r;
+  asm volatile("global_load_dwordx4 %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  return r;
 }
 
 // Item k of this block covers vectors (k * G + part) * 64 + lane; `body(x, v)`
@@ -592,12 +623,13 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
   constexpr int C = kBlock / 64 - 1;
   static_assert(C >= 1, "a consumer wave");
   __shared__ v4u ring[S * NIN * R * 64];
-  __shared__ unsigned full[S], freed[S];
+  __shared__ unsigned full[S], freed[S], bypass;
   // every wave has left the ring's previous use (a kernel looping over jobs
   // calls this once per job: the loader finishes a job first and must not
   // reset flags that consumers of that job still poll)
   __syncthreads();
   if (threadIdx.x < S) full[threadIdx.x] = 0, freed[threadIdx.x] = 0;
+  if (threadIdx.x == 0) bypass = 0;
   __syncthreads();
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
@@ -623,7 +655,17 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
 #endif
         unsigned spins = 0;
         while (ring_flag_ld(&freed[k % S]) < use && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
-        if (spins >= kRingSpinCap && lane == 0 && fault) atomicAdd(fault, 1u);
+        if (spins >= kRingSpinCap) {
+          // a consumer still holds the slot: leave it alone, hand every item
+          // not yet published to its consumer's direct loads, and stop
+          ring_wait_vm<0>();
+          while (pub < k) publish();
+          if (lane == 0) {
+            ring_flag_st(&bypass, 1u);
+            if (fault) atomicAdd(fault, 1u);
+          }
+          return;
+        }
       }
       const uint32_t slot = ring0 + static_cast<uint32_t>((k % S) * NIN * R * 1024);
 #pragma unroll
@@ -656,16 +698,42 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
   for (size_t k = wave - 1; k < K; k += C) {
     const unsigned want = static_cast<unsigned>(k / S) + 1;
     unsigned spins = 0;
-    while (ring_flag_ld(&full[k % S]) < want && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(REDSET_RING_SLEEP);
-    if (spins >= kRingSpinCap && lane == 0 && fault) atomicAdd(fault, 1u);
-    const lr_u4* sl = (const lr_u4*) ring + (k % S) * NIN * R * 64;
+    bool direct = false;
+    while (ring_flag_ld(&full[k % S]) < want) {
+      if (ring_flag_ld(&bypass) != 0u || ++spins >= kRingSpinCap) {
+        direct = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(REDSET_RING_SLEEP);
+    }
     v4u x[R][NIN];
+    if (!direct) {
+      const lr_u4* sl = (const lr_u4*) ring + (k % S) * NIN * R * 64;
 #pragma unroll
-    for (int r = 0; r < R; ++r)
+      for (int r = 0; r < R; ++r)
 #pragma unroll
-      for (int i = 0; i < NIN; ++i) x[r][i] = sl[(i * R + r) * 64 + lane];
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    if (lane == 0) ring_flag_st(&freed[k % S], want);
+        for (int i = 0; i < NIN; ++i) x[r][i] = sl[(i * R + r) * 64 + lane];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) ring_flag_st(&freed[k % S], want);
+    } else {
+      // the item never arrived in time (or the loader stopped): take this
+      // lane's bytes from HBM; the ring copy, if it ever lands, is unread.
+      // Release the slot for item k + S only after item k - S's consumer
+      // has (FREE = want - 1), or the loader could overwrite a slot that
+      // consumer still reads; if that never happens the loader's own capped
+      // wait raises BYPASS.
+      if (spins >= kRingSpinCap && lane == 0 && fault) atomicAdd(fault, 1u);
+      unsigned s2 = 0;
+      while (ring_flag_ld(&freed[k % S]) + 1u < want && ++s2 < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+      if (lane == 0 && ring_flag_ld(&freed[k % S]) + 1u >= want) ring_flag_st(&freed[k % S], want);
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const size_t v = vec_of(k, r);
+        const size_t vc = v < nvec ? v : nvec - 1;
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) x[r][i] = ring_direct_load(in[i] + vc);
+      }
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       const size_t v = vec_of(k, r);
@@ -744,7 +812,12 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
     for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (J.in[i]);
     g_u4* out = (g_u4*) (J.out);
 #if REDSET_RING
-    ring_sweep<NIN, REDSET_RING_XOR_ROWS, REDSET_RING_XOR_DEPTH>(
+    // two-row items hold 2 * NIN input vectors per lane: past 8 inputs that
+    // no longer fits 1024-thread blocks' 128 VGPRs, so wide XOR sets take
+    // the GF kernels' one-row shape
+    constexpr int kRows = NIN > REDSET_RING_XOR_WIDE ? 1 : REDSET_RING_XOR_ROWS;
+    constexpr int kDepth = NIN > REDSET_RING_XOR_WIDE ? REDSET_RING : REDSET_RING_XOR_DEPTH;
+    ring_sweep<NIN, kRows, kDepth>(
         in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
         [&](const v4u (&x)[NIN], size_t v) { xor_vec<NIN, ACC>(x, out, v, true); });
 #else

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 
 #include "codec_kernels.h"
 
@@ -37,18 +38,25 @@ int jobs_per_launch(const Launch& L) {
 }
 
 // Capped loader-ring spins (codec_device.h ring_sweep), one word per device:
-// the kernels get its address in GfLaunch / XorLaunch::fault.
+// the kernels get its address in GfLaunch / XorLaunch::fault. Launches come
+// from several threads (the pipeline's compute thread, per-rank backends,
+// callers), so the per-device address cache is atomic; a racing first
+// lookup resolves the same address twice, which is harmless.
 __device__ unsigned g_ring_fault;
 
 unsigned* ring_fault_word() {
-  static unsigned* addr[64] = {};
+  static std::atomic<unsigned*> addr[64];
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!addr[dev]) {
+  unsigned* a = addr[dev].load(std::memory_order_acquire);
+  if (!a) {
     void* p = nullptr;
-    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_ring_fault)) == hipSuccess) addr[dev] = static_cast<unsigned*>(p);
+    if (hipGetSymbolAddress(&p, HIP_SYMBOL(g_ring_fault)) == hipSuccess) {
+      a = static_cast<unsigned*>(p);
+      addr[dev].store(a, std::memory_order_release);
+    }
   }
-  return addr[dev];
+  return a;
 }
 }  // namespace
 

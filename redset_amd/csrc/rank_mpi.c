@@ -847,9 +847,11 @@ static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream
         return fail("mpi transport: hipHostMalloc(%zu) failed", need);
       T->stage_len = need;
     }
-    /* work already on the stream produced the send buffers */
-    if (hipStreamSynchronize(s) != hipSuccess) return fail("mpi transport: stream sync failed");
   }
+  /* work already on the stream produced the send buffers -- in host mode
+   * too, where a HIP compute over page-locked slabs may still be writing
+   * them (a host-only caller passes no stream and needs no HIP runtime) */
+  if ((T->device || s) && hipStreamSynchronize(s) != hipSuccess) return fail("mpi transport: stream sync failed");
   if ((int) nreq > T->req_cap) {
     MPI_Request* r = realloc(T->req, sizeof(*r) * nreq);
     if (!r) return fail("out of host memory");

@@ -33,11 +33,21 @@ def oracle():
     return oracle_lib
 
 
+# REDSET_RING_FALLBACK_RUN=1: the suite runs against the spin-cap twin of the
+# library (tests/test_gpu_ring_fallback.py), whose ring handshakes give up on
+# purpose; capped spins are then expected, counted and written to
+# REDSET_RING_FAULT_LOG instead of failing the test.
+FALLBACK_RUN = os.environ.get("REDSET_RING_FALLBACK_RUN") == "1"
+_fallback_faults = [0]
+
+
 @pytest.fixture(autouse=True)
 def _no_ring_faults(request):
     """After every GPU test that used the codec in this process: no kernel's
-    loader-ring handshake hit its spin cap (codec_device.h ring_sweep; a
-    capped spin means wrong outputs, so it fails the test loudly)."""
+    loader-ring handshake hit its spin cap (codec_device.h ring_sweep). A
+    capped spin falls back to direct HBM loads, so outputs stay right (the
+    tests' byte comparisons say so), but in the shipped build it means the
+    ring stalled for 2^24 polls, which is a bug to find."""
     yield
     if request.node.get_closest_marker("gpu") is None:
         return
@@ -47,4 +57,18 @@ def _no_ring_faults(request):
         return
     import redset_amd
 
-    assert redset_amd.ring_faults() == 0, "a loader-ring handshake hit its spin cap"
+    n = redset_amd.ring_faults()
+    if FALLBACK_RUN:
+        _fallback_faults[0] += n
+        return
+    assert n == 0, "a loader-ring handshake hit its spin cap"
+
+
+def pytest_sessionfinish(session, exitstatus):
+    log = os.environ.get("REDSET_RING_FAULT_LOG")
+    if FALLBACK_RUN and log:
+        # which codec libraries this process actually mapped
+        with open("/proc/self/maps") as m:
+            libs = sorted({ln.split()[-1] for ln in m if ln.rstrip().endswith("libredset_hip.so")})
+        with open(log, "w") as f:
+            f.write(f"{_fallback_faults[0]}\n" + "".join(f"{x}\n" for x in libs))

@@ -1,6 +1,6 @@
 /* TEST-ONLY: the one KVTree name redset's headers use (an opaque type), for
- * the adapter's syntax check (tests/test_integration_adapter.py). KVTree
- * itself is an absent third-party dependency; nothing links against this. */
+ * compiling the adapter (tests/test_integration_adapter.py, tests/adapter/).
+ * KVTree itself is an absent third-party dependency; nothing calls into it. */
 #ifndef KVTREE_H
 #define KVTREE_H
 typedef struct kvtree_struct kvtree;

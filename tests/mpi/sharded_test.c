@@ -7,13 +7,17 @@
  * slicing and both exchanges are checked against the oracle's whole-set
  * encode / rebuild without a GPU.
  *
- * usage: sharded_test [--gpu] <p> <e> <chunk> [lost ranks...]   (world = MPI size)
+ * usage: sharded_test [--gpu | --gpu-host] <p> <e> <chunk> [lost ranks...]   (world = MPI size)
  * SHARDED_TEST_REPS=<n> (--gpu): after the checks, time n rebuilds with the
  * pipelined execute and n with the three phases one after another (slowest
  * process, ms per rebuild).
  * --gpu: the slabs live in HBM, the compute is the HIP gf_mac plans and the
  * MPI transport stages through pinned host memory (every process may share
  * one GPU) -- the whole sharded path with the real kernels at world > 1.
+ * --gpu-host: the slabs live in page-locked host memory, the compute is the
+ * HIP gf_mac plans reading and writing them in place, and the MPI transport
+ * works on the host buffers directly -- it must wait for the kernels that
+ * wrote a return exchange's slices before it sends them.
  * Placement: `world` sets of p members, member m on process (m * 7 + 3) %
  * world (SHARDED_TEST_SEED=<s>: on a pseudo-random process), hosted slots in
  * ascending member order. Exit 0 iff every process
@@ -40,6 +44,22 @@ static uint8_t byte_of(int k, int r, size_t i) { /* member (k, r)'s logical-file
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ULL;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBULL;
   return (uint8_t) (z ^ (z >> 31));
+}
+
+/* slab copies: hipMemcpy / hipMemset for HBM slabs, plain memory ops for
+ * page-locked host slabs (after the stream's kernels are done with them) */
+static int HOST_SLABS;
+static int to_slab(void* dst, const void* src, size_t n) {
+  if (HOST_SLABS) return memcpy(dst, src, n), 0;
+  return hipMemcpy(dst, src, n, hipMemcpyHostToDevice) != hipSuccess;
+}
+static int from_slab(void* dst, const void* src, size_t n) {
+  if (HOST_SLABS) return memcpy(dst, src, n), 0;
+  return hipMemcpy(dst, src, n, hipMemcpyDeviceToHost) != hipSuccess;
+}
+static int fill_slab(void* dst, int v, size_t n) {
+  if (HOST_SLABS) return memset(dst, v, n), 0;
+  return hipMemset(dst, v, n) != hipSuccess;
 }
 
 /* compute callback: the oracle on compacted copies of the slices */
@@ -72,7 +92,9 @@ int main(int argc, char** argv) {
   int world, me;
   MPI_Comm_size(MPI_COMM_WORLD, &world);
   MPI_Comm_rank(MPI_COMM_WORLD, &me);
-  const int gpu = argc > 1 && strcmp(argv[1], "--gpu") == 0;
+  const int host_slabs = argc > 1 && strcmp(argv[1], "--gpu-host") == 0;
+  const int gpu = host_slabs || (argc > 1 && strcmp(argv[1], "--gpu") == 0);
+  HOST_SLABS = host_slabs;
   if (gpu) {
     --argc;
     ++argv;
@@ -130,7 +152,22 @@ int main(int argc, char** argv) {
   redset_hip_shard_layout L = {nsets, host, slot, mh, C, W, HD, HP, GD, GP};
   uint8_t *dHD = NULL, *dHP = NULL, *dGD = NULL, *dGP = NULL;
   hipStream_t stream = NULL;
-  if (gpu) {
+  if (host_slabs) {
+    /* every slab page-locked; kernels and MPI use the same addresses */
+    if (hipHostMalloc((void**) &dHD, hd, 0) || hipHostMalloc((void**) &dHP, hp, 0) ||
+        hipHostMalloc((void**) &dGD, hd, 0) || hipHostMalloc((void**) &dGP, hp, 0) || hipStreamCreate(&stream)) {
+      fprintf(stderr, "rank %d: pinned setup failed\n", me);
+      MPI_Abort(MPI_COMM_WORLD, 3);
+    }
+    memcpy(dHD, HD, hd);
+    memset(dHP, 0, hp);
+    memset(dGD, 0, hd);
+    memset(dGP, 0, hp);
+    L.hosted_data = dHD;
+    L.hosted_parity = dHP;
+    L.gathered_data = dGD;
+    L.gathered_parity = dGP;
+  } else if (gpu) {
     if (hipMalloc((void**) &dHD, hd) || hipMalloc((void**) &dHP, hp) || hipMalloc((void**) &dGD, hd) ||
         hipMalloc((void**) &dGP, hp) || hipStreamCreate(&stream) || hipMemcpy(dHD, HD, hd, hipMemcpyHostToDevice) ||
         hipMemset(dHP, 0, hp) || hipMemset(dGD, 0, hd) || hipMemset(dGP, 0, hp)) {
@@ -144,7 +181,7 @@ int main(int argc, char** argv) {
   }
   redset_hip_sharded *enc = NULL, *reb = NULL;
   const redset_hip_compute* cp = gpu ? NULL : &comp;
-  int ok = redset_hip_rs_create(P, E, &rs) == 0 && redset_hip_mpi_transport_create(MPI_COMM_WORLD, gpu, &tr, &th) == 0 &&
+  int ok = redset_hip_rs_create(P, E, &rs) == 0 && redset_hip_mpi_transport_create(MPI_COMM_WORLD, gpu && !host_slabs, &tr, &th) == 0 &&
            redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, &tr, cp, &enc) == 0 &&
            (missing == 0 ||
             redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, &tr, cp, &reb) == 0);
@@ -154,7 +191,7 @@ int main(int argc, char** argv) {
     fprintf(stderr, "rank %d: encode: %s\n", me, redset_hip_last_error());
     ok = 0;
   }
-  if (gpu && (hipStreamSynchronize(stream) || hipMemcpy(HP, dHP, hp, hipMemcpyDeviceToHost))) ok = 0;
+  if (gpu && (hipStreamSynchronize(stream) || from_slab(HP, dHP, hp))) ok = 0;
   /* compare my hosted members' parity slabs with the oracle */
   for (int m = 0; ok && m < nm; ++m) {
     if (host[m] != me) continue;
@@ -177,15 +214,13 @@ int main(int argc, char** argv) {
     }
     memset(GD, 0xA5, hd);
     memset(GP, 0x5A, hp);
-    if (gpu && (hipMemcpy(dHD, HD, hd, hipMemcpyHostToDevice) || hipMemcpy(dHP, HP, hp, hipMemcpyHostToDevice) ||
-                hipMemset(dGD, 0xA5, hd) || hipMemset(dGP, 0x5A, hp)))
+    if (gpu && (to_slab(dHD, HD, hd) || to_slab(dHP, HP, hp) || fill_slab(dGD, 0xA5, hd) || fill_slab(dGP, 0x5A, hp)))
       ok = 0;
     if (ok && redset_hip_sharded_execute(reb, stream) != 0) {
       fprintf(stderr, "rank %d: rebuild: %s\n", me, redset_hip_last_error());
       ok = 0;
     }
-    if (gpu && (hipStreamSynchronize(stream) || hipMemcpy(HD, dHD, hd, hipMemcpyDeviceToHost) ||
-                hipMemcpy(HP, dHP, hp, hipMemcpyDeviceToHost)))
+    if (gpu && (hipStreamSynchronize(stream) || from_slab(HD, dHD, hd) || from_slab(HP, dHP, hp)))
       ok = 0;
     int rbad = 0;
     for (int m = 0; ok && m < nm; ++m) {
@@ -227,7 +262,13 @@ int main(int argc, char** argv) {
   redset_hip_sharded_destroy(reb);
   redset_hip_mpi_transport_destroy(th);
   redset_hip_rs_destroy(rs);
-  if (gpu) {
+  if (host_slabs) {
+    (void) hipHostFree(dHD);
+    (void) hipHostFree(dHP);
+    (void) hipHostFree(dGD);
+    (void) hipHostFree(dGP);
+    (void) hipStreamDestroy(stream);
+  } else if (gpu) {
     (void) hipFree(dHD);
     (void) hipFree(dHP);
     (void) hipFree(dGD);

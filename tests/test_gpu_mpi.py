@@ -157,18 +157,22 @@ def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme
     assert "Sanitizer" not in res.stderr, res.stderr[-4000:]  # tools/gpu_asan.sh builds
 
 
+@pytest.mark.parametrize("mode", ["--gpu", "--gpu-host"])
 @pytest.mark.parametrize("np_,p,e,chunk,lost", [(2, 11, 3, 300_001, [1, 2]), (4, 20, 4, 65536, [0, 5, 19]),
                                                  (3, 6, 3, 1000, [2])])
-def test_mpi_sharded_gpu(np_, p, e, chunk, lost):
-    """The sharded path with the real HIP kernels at world > 1: slabs in HBM,
-    gf_mac plans over each process's column slice, the MPI transport staging
-    through pinned memory (the processes share the box's one GPU; RCCL needs
-    one GPU per rank). tests/mpi/sharded_test.c --gpu checks hosted parity and
-    the rebuilt members against the oracle."""
+def test_mpi_sharded_gpu(np_, p, e, chunk, lost, mode):
+    """The sharded path with the real HIP kernels at world > 1: gf_mac plans
+    over each process's column slice (the processes share the box's one GPU;
+    RCCL needs one GPU per rank). --gpu: slabs in HBM, the MPI transport
+    staging through pinned memory. --gpu-host: slabs in page-locked host
+    memory that the kernels read and write in place and MPI sends directly,
+    so the transport must wait for the stream's kernels before a return
+    exchange (rank_mpi.c mpi_exchange). tests/mpi/sharded_test.c
+    checks hosted parity and the rebuilt members against the oracle."""
     driver = os.environ.get("SHARDED_TEST_BIN") or os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
     if not _have() or not os.path.exists(driver):
         pytest.skip("needs a GPU, MPICH and tests/mpi/build/sharded_test")
-    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", driver, "--gpu", str(p), str(e), str(chunk)] + \
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", driver, mode, str(p), str(e), str(chunk)] + \
         [str(x) for x in lost]
     res = run_group(cmd, 120)
     assert res.returncode == 0, res.stdout + res.stderr
@@ -213,8 +217,10 @@ def test_mpi_config0_xor_4_ranks_16MiB(oracle, tmp_path):
 @pytest.mark.parametrize("seed", range(6))
 def test_mpi_sharded_gpu_random(seed):
     """tests/test_mpi_sharded.py's random shapes and placements with the HIP
-    kernels and the pipelined execute (slabs in HBM, MPI transport staging
-    through pinned memory; the processes share the box's GPU)."""
+    kernels and the pipelined execute (even seeds: slabs in HBM, MPI
+    transport staging through pinned memory; odd seeds: page-locked host
+    slabs; the processes share the box's GPU)."""
+    mode = "--gpu-host" if seed % 2 else "--gpu"
     driver = os.environ.get("SHARDED_TEST_BIN") or os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
     if not _have() or not os.path.exists(driver):
         pytest.skip("needs a GPU, MPICH and tests/mpi/build/sharded_test")
@@ -225,7 +231,7 @@ def test_mpi_sharded_gpu_random(seed):
     chunk = int(rng.choice([1, 255, 257, int(rng.integers(2, 200_000))]))
     m = int(rng.integers(1, e + 1))
     lost = sorted(rng.choice(p, size=m, replace=False).tolist())
-    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", driver, "--gpu", str(p), str(e), str(chunk)] + \
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", driver, mode, str(p), str(e), str(chunk)] + \
         [str(x) for x in lost]
     res = run_group(cmd, 120, env={**os.environ, "SHARDED_TEST_SEED": str(seed)})
     assert res.returncode == 0, (np_, p, e, chunk, lost, res.stdout + res.stderr)

@@ -42,13 +42,15 @@
 #define REDSET_MEMONLY 0
 #endif
 // Table offsets of the GF lookups: 0 = packed shift + mask, then one extract
-// per offset (12 VALU ops per input dword); 1 = one SDWA-byte-select AND per
-// offset (10 ops); 2 (default) = SDWA only in kernels with <= 2 outputs. The
-// fixed per-position cost weighs most where few output bytes amortise it:
-// SDWA gains 3.8% on the 2-output rebuild and loses 0.6% on the 3-output
-// encode, so 2 = +1.9% on the RS step (profiles/r01_ab_sdwa_offsets.txt).
+// per offset (12 VALU ops per input dword); 1 (default) = one SDWA-byte-select
+// AND per offset (10 ops); 2 = SDWA only in kernels with <= 2 outputs. Round
+// 1 measured 2 best (+1.9% on the RS step; SDWA cost the 3-output encode
+// 0.6%, profiles/r01_ab_sdwa_offsets.txt) -- while every lookup also paid a
+// v_add of the tables' LDS base. With the tables at the bottom of LDS
+// (gf_mac_body), 1 is ahead: +0.7% encode, +0.6% step over 2
+// (profiles/r03_ab_tables_first.txt).
 #ifndef REDSET_SDWA_OFFSETS
-#define REDSET_SDWA_OFFSETS 2
+#define REDSET_SDWA_OFFSETS 1
 #endif
 // knob 2: the SDWA parts (sdwa_parts) of the kernels with > 2 outputs
 #ifndef REDSET_SDWA_WIDE_PARTS
@@ -122,6 +124,17 @@ __device__ __forceinline__ uint32_t gf_mul_dev(uint32_t a, uint32_t b) {
 // one op per input dword fewer than (w >> 2) & 0x3C3C3C3C, but measured 2.8%
 // slower on the rebuild (profiles/r01_ab_sdwa_offsets.txt), so 4 stays (A/B
 // knob; both strides keep the 16 entries in 16 distinct LDS banks).
+// REDSET_HI_B64 = 1: high-nibble entries 16 B apart (offset = byte & 0xF0,
+// one SDWA op and no shift) read with ds_read_b64, whose banks are (a/4) mod
+// 64, so the 16 entries stay conflict-free (as ds_read_b32 they would pair
+// up 2-way); the upper dword is unused.
+#ifndef REDSET_HI_B64
+#define REDSET_HI_B64 0
+#endif
+#if REDSET_HI_B64
+#undef REDSET_HI_STRIDE
+#define REDSET_HI_STRIDE 16
+#endif
 #ifndef REDSET_HI_STRIDE
 #define REDSET_HI_STRIDE 4
 #endif
@@ -197,6 +210,18 @@ __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
 // dword at byte offset `off` of the LDS image
 __device__ __forceinline__ uint32_t lds_at(const uint32_t* lds, uint32_t off) {
   return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const char*>(lds) + off);
+}
+
+// high-nibble table entry at byte offset `off` (REDSET_HI_B64: a 64-bit read)
+__device__ __forceinline__ uint32_t lds_hi_at(const uint32_t* lds, uint32_t off) {
+#if REDSET_HI_B64
+  typedef unsigned int u2 __attribute__((ext_vector_type(2)));
+  typedef __attribute__((address_space(3))) const volatile u2 lds_u2;
+  // volatile: a plain read whose upper half is unused is narrowed to ds_read_b32
+  return ((lds_u2*) (reinterpret_cast<const char*>(lds) + off))->x;
+#else
+  return lds_at(lds, off);
+#endif
 }
 
 // gather byte j of a[0..3] into one dword
@@ -282,7 +307,7 @@ __device__ __forceinline__ void gf_acc_input(const uint32_t* lds, const v4u& x, 
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       acc[4 * q + b] = xor3(acc[4 * q + b], lds_at(lds, i * kTableBytes + ol[b]),
-                            lds_at(lds, i * kTableBytes + kHiBase + oh[b]));
+                            lds_hi_at(lds, i * kTableBytes + kHiBase + oh[b]));
     }
   }
 }
@@ -580,6 +605,10 @@ constexpr int kRingBudget = REDSET_RING_KIB * 1024;
 #ifndef REDSET_RING_SLEEP
 #define REDSET_RING_SLEEP 8
 #endif
+// s_setprio of the loader wave (A/B knob, 0 = same priority as consumers)
+#ifndef REDSET_RING_LOADER_PRIO
+#define REDSET_RING_LOADER_PRIO 0
+#endif
 #ifndef REDSET_RING_MAX_SLOTS
 #define REDSET_RING_MAX_SLOTS 16
 #endif
@@ -615,14 +644,21 @@ __device__ __forceinline__ v4u ring_direct_load(g_cu4* p) {
 
 // Item k of this block covers vectors (k * G + part) * 64 + lane; `body(x, v)`
 // combines and stores one in-range vector position.
+// LDS the ring of a kernel with NIN inputs and R-row items occupies (v4u)
+template <int NIN, int R>
+constexpr int ring_vecs() {
+  return ring_slots<NIN * R>() * NIN * R * 64;
+}
+
+// `ring` is LDS storage of ring_vecs<NIN, R>() vectors, declared by the
+// caller (gf_mac puts its GF tables in front of it, see gf_mac_body).
 template <int NIN, int R, int D, typename Body>
-__device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec, size_t G, size_t part,
+__device__ __forceinline__ void ring_sweep(v4u* ring, g_cu4* const (&in)[NIN], size_t nvec, size_t G, size_t part,
                                            unsigned* fault, Body body) {
   constexpr int S = ring_slots<NIN * R>();
   static_assert(D >= 1 && D - 1 < S && (D - 1) * NIN * R <= 63, "ring depth");
   constexpr int C = kBlock / 64 - 1;
   static_assert(C >= 1, "a consumer wave");
-  __shared__ v4u ring[S * NIN * R * 64];
   __shared__ unsigned full[S], freed[S], bypass;
   // every wave has left the ring's previous use (a kernel looping over jobs
   // calls this once per job: the loader finishes a job first and must not
@@ -639,6 +675,7 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
   // vector of row r of item k in this block
   auto vec_of = [&](size_t k, int r) { return ((k * G + part) * R + r) * 64 + lane; };
   if (wave == 0) {
+    if constexpr (REDSET_RING_LOADER_PRIO > 0) __builtin_amdgcn_s_setprio(REDSET_RING_LOADER_PRIO);
     const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lr_u4*) ring)));
     // items [pub, k) are issued and not yet published
     size_t pub = 0;
@@ -745,8 +782,19 @@ __device__ __forceinline__ void ring_sweep(g_cu4* const (&in)[NIN], size_t nvec,
 
 template <int NIN, int NOUT, bool ACC>
 __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, int part) {
-  // static (not extern) so the table offsets fold into ds_read's immediate
-  __shared__ uint32_t lds[kMaxIn * kTableBytes / 4];
+  // One static LDS array, the GF tables first and the loader ring behind
+  // them: the tables' addresses (< 2 KiB) then fold into ds_read's 16-bit
+  // immediate offset, so a lookup's address is the table offset alone. As two
+  // arrays the compiler put the 128 KiB ring first, and every lookup paid a
+  // v_add of the tables' base (0x20000) -- 4 of ~20 VALU ops per input dword.
+  constexpr int kTableVecs = kMaxIn * kTableBytes / 16;
+#if REDSET_RING
+  constexpr int kRingVecs = ring_vecs<NIN, REDSET_RING_GF_ROWS>();
+#else
+  constexpr int kRingVecs = 0;
+#endif
+  __shared__ v4u smem[kTableVecs + kRingVecs];
+  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem);
 
   build_tables(lds, J, NIN, NOUT);
   __syncthreads();
@@ -762,7 +810,7 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
     for (int j = 0; j < NOUT; ++j) out[j] = (g_u4*) (J.out[j]);
 #if REDSET_RING
     ring_sweep<NIN, REDSET_RING_GF_ROWS, REDSET_RING>(
-        in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
+        smem + kTableVecs, in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
         [&](const v4u (&x)[NIN], size_t v) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, true); });
 #elif REDSET_GLDS
     __shared__ v4u ring_mem[glds_stages<NIN>() * NIN * 64 * kWavesPerBlock];
@@ -817,8 +865,9 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
     // the GF kernels' one-row shape
     constexpr int kRows = NIN > REDSET_RING_XOR_WIDE ? 1 : REDSET_RING_XOR_ROWS;
     constexpr int kDepth = NIN > REDSET_RING_XOR_WIDE ? REDSET_RING : REDSET_RING_XOR_DEPTH;
+    __shared__ v4u ring[ring_vecs<NIN, kRows>()];
     ring_sweep<NIN, kRows, kDepth>(
-        in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
+        ring, in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
         [&](const v4u (&x)[NIN], size_t v) { xor_vec<NIN, ACC>(x, out, v, true); });
 #else
     sweep<NIN, sweep_prio(3)>(

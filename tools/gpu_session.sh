@@ -39,3 +39,9 @@ timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/pmc_wr
 s=$?; echo "pmc write exit $s" | tee -a "$OUT/progress.txt"; ok $s || exit $s
 python3 tools/pmc_traffic.py "$OUT/pmc_fetch" "$OUT/pmc_write" "$OUT/traffic.json" > /dev/null
 echo "== done" | tee -a "$OUT/progress.txt"
+echo "== N=2 gloo rehearsal of bench.py --gpus 2 (both ranks on the one GPU)" | tee -a "$OUT/progress.txt"
+timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+  --master-port 29533 bench.py --gpus 2 --dist-backend gloo --chunk-mib 2 --steps 3 --warmup 1 \
+  --cpu-baseline 0 --pairs 0 > "$OUT/n2_gloo.json" 2> "$OUT/n2_gloo.err"
+s=$?; echo "n2 gloo exit $s" | tee -a "$OUT/progress.txt"; ok $s || exit $s
+echo "== done (gloo)" | tee -a "$OUT/progress.txt"

@@ -82,6 +82,15 @@ int redset_hip_rs_get_data_id(int ranks, int encoding, int rank, int chunk_id);
 
 /* ---- whole-set plans (all members' cells resident on one device) ----- */
 
+/* Recommended cell_stride for a set held in one device allocation: chunk_size
+ * rounded up to 256 B, plus 16 MiB when that is a multiple of 16 MiB. Cells
+ * of a power-of-two size such as 64 MiB otherwise start at addresses equal
+ * modulo 2^24..2^26, and a stripe's 11 streams then share DRAM channels and
+ * banks; the pad staggers them (+2.0% on the RS(8+3) step at 64 MiB cells,
+ * profiles/r02_ab_cell_pad.txt; the bench uses this layout). Any stride >=
+ * chunk_size is correct; this one is only faster. */
+size_t redset_hip_cell_stride(size_t chunk_size);
+
 /* Parity of every stripe of the set: the work redset_reedsolomon_encode
  * (src/redset_reedsolomon.c:280-402) does across all p ranks; member r's
  * parity slot i = stripe (r+i) mod p, row p+i. lofi/parity: p device pointers. */

@@ -14,6 +14,7 @@ from .codec import (  # noqa: F401
     RSCodec,
     SetLayout,
     gf_combine,
+    cell_stride,
     ring_faults,
     xor_combine,
     xor_plan_encode,

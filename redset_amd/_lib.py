@@ -31,6 +31,7 @@ EXPORTED_SYMBOLS = (
     "redset_hip_rs_shape",
     "redset_hip_rs_get_encoding_id",
     "redset_hip_rs_get_data_id",
+    "redset_hip_cell_stride",
     "redset_hip_rs_plan_encode",
     "redset_hip_rs_plan_rebuild",
     "redset_hip_xor_plan_encode",
@@ -180,6 +181,7 @@ _SIGNATURES = {
     "redset_hip_rs_shape": (c_int, [c_void_p, POINTER(c_int), POINTER(c_int)]),
     "redset_hip_rs_get_encoding_id": (c_int, [c_int, c_int, c_int, c_int]),
     "redset_hip_rs_get_data_id": (c_int, [c_int, c_int, c_int, c_int]),
+    "redset_hip_cell_stride": (c_size_t, [c_size_t]),
     "redset_hip_rs_plan_encode": (c_int, [c_void_p, _PP, _PP, c_size_t, c_size_t, POINTER(c_void_p)]),
     "redset_hip_rs_plan_rebuild": (
         c_int,

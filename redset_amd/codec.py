@@ -257,6 +257,12 @@ class SetLayout:
         return [self.parity(r).data_ptr() for r in range(self.ranks)]
 
 
+def cell_stride(chunk_size: int) -> int:
+    """The library's recommended cell stride for a set held in one
+    allocation (include/redset_hip.h redset_hip_cell_stride)."""
+    return int(_lib.load().redset_hip_cell_stride(chunk_size))
+
+
 def ring_faults(clear: bool = True) -> int:
     """Capped loader-ring handshake spins on the current device since the
     last clearing read (include/redset_hip.h redset_hip_ring_faults). Outputs

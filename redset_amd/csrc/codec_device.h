@@ -345,7 +345,7 @@ __device__ __forceinline__ void gf_mac_vec(const uint32_t* lds, const v4u (&x)[N
     if constexpr (ACC) {
       if (store) out[j][v] = m ^ out[j][v];
     } else {
-      out[j][v] = m + j;
+      store_vec(out[j], v, m + j);  // the real kernel's store policy
     }
   }
   return;

@@ -415,6 +415,14 @@ int redset_hip_rs_decode_matrix(const redset_hip_rs* rs, int missing, const int*
   return REDSET_SUCCESS;
 }
 
+size_t redset_hip_cell_stride(size_t chunk_size) {
+  constexpr size_t kAlign = 256, kPad = size_t(16) << 20;
+  size_t stride = (chunk_size + kAlign - 1) / kAlign * kAlign;
+  if (stride == 0) stride = kAlign;
+  if (stride % kPad == 0) stride += kPad;
+  return stride;
+}
+
 int redset_hip_rs_plan_encode(const redset_hip_rs* rs, unsigned char* const* lofi, unsigned char* const* parity,
                               size_t chunk_size, size_t stride, redset_hip_plan** out) {
   if (!rs) return fail("null rs state");

@@ -202,3 +202,17 @@ def test_bad_arguments_rejected_before_any_device_work(hiplib):
     assert L.redset_hip_xor_combine(as_pp(nul), 2, 16, 64, 0, None) == 1
     assert b"null input 1" in L.redset_hip_last_error()
     assert L.redset_hip_xor_combine(as_pp(ptrs), 2, None, 64, 0, None) == 1
+
+
+def test_cell_stride_recommendation(hiplib):
+    """redset_hip_cell_stride: 256-B aligned, >= chunk, and a 16 MiB stagger
+    for 16 MiB-multiple cells (the bench's 64 MiB layout)."""
+    f = hiplib.cell_stride
+    MiB = 1 << 20
+    assert f(0) == 256 and f(1) == 256 and f(256) == 256 and f(257) == 512
+    assert f(5592406) == 5592576                      # configs[0]'s chunk: aligned, no pad
+    assert f(64 * MiB) == 80 * MiB                    # configs[1]-[3]
+    assert f(256 * MiB) == 272 * MiB                  # configs[4]
+    assert f(16 * MiB) == 32 * MiB and f(16 * MiB + 1) == 16 * MiB + 256
+    for c in (1, 4095, 3 * MiB + 7, 48 * MiB):
+        assert f(c) >= c and f(c) % 256 == 0

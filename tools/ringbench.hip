@@ -17,6 +17,7 @@
 // it waits for a free slot, so every issued item is eventually published.
 // Every spin is bounded (kSpinCap); a capped spin sets an error flag.
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/ringbench tools/ringbench.hip
+// Run: ringbench [reps] [rand]
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
@@ -162,6 +163,16 @@ __global__ void __launch_bounds__(kBlock) kring(Stripe J, size_t nvec, unsigned*
   }
 }
 
+// uniform random bytes (splitmix64 of the dword index), like the bench's cells
+__global__ void kfill_random(unsigned* p, size_t n, unsigned long long seed) {
+  for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t) gridDim.x * blockDim.x) {
+    unsigned long long z = (seed + i) * 0x9E3779B97F4A7C15ull;
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    p[i] = (unsigned) (z ^ (z >> 31));
+  }
+}
+
 __global__ void kcount_diff(const v4u* a, const v4u* b, size_t n, unsigned long long* bad) {
   unsigned long long local = 0;
   for (size_t i = (size_t) blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t) gridDim.x * blockDim.x) {
@@ -180,8 +191,15 @@ int main(int argc, char** argv) {
   unsigned char* base = nullptr;
   CK(hipMalloc(&base, ncell * stride + 3 * cell));
   CK(hipMemset(base, 0x5A, ncell * stride));
-  // distinct input contents: byte pattern per cell
-  for (size_t c = 0; c < ncell; ++c) CK(hipMemset(base + c * stride, (int) (c * 37 + 11) & 0xFF, cell / 2));
+  // distinct input contents: byte pattern per cell, or (argv[2] = "rand")
+  // uniform random bytes in every cell, as the codec bench uses
+  const bool rnd = argc > 2 && argv[2][0] == 'r';
+  for (size_t c = 0; c < ncell; ++c) {
+    if (rnd) kfill_random<<<1024, 256>>>((unsigned*) (base + c * stride), cell / 4, c << 40);
+    else CK(hipMemset(base + c * stride, (int) (c * 37 + 11) & 0xFF, cell / 2));
+  }
+  CK(hipDeviceSynchronize());
+  printf("inputs: %s\n", rnd ? "uniform random" : "constant halves");
   std::vector<Stripe> js(nstripe);
   for (int s = 0; s < nstripe; ++s) {
     for (int i = 0; i < NIN; ++i) js[s].in[i] = (gcv4*) (base + ((size_t) s * (NIN + NOUT) + i) * stride);

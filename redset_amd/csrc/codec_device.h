@@ -60,10 +60,16 @@
 // exactly once, so both directions are marked non-temporal (`nt`): +3% on
 // the RS step and +7% on XOR against the default policy, while either one
 // alone gains nothing (nt loads alone lose 2%) -- profiles/r01_ab_cache_policy.txt.
-// A/B knobs (tools/build_ab_variant.sh): stores 0 = default, 1 = nt,
-// 2 = sc0 sc1 nt, 3 = sc1 nt, 4 = sc0 nt, 5 = sc0 sc1; loads 0 = default, 1 = nt.
+// A/B knobs (tools/build_ab_variant.sh): stores 0 = default, 1 = nt; loads
+// 0 = default, 1 = nt. (Round 1 also tried sc0/sc1 variants as inline-asm
+// stores; with the ring kernels those builds failed the bench's round trip,
+// profiles/r03_ab_cache_policy.txt -- the compiler does not protect an asm
+// store's data registers -- so they are gone.)
 #ifndef REDSET_STORE_POLICY
 #define REDSET_STORE_POLICY 1
+#endif
+#if REDSET_STORE_POLICY != 0 && REDSET_STORE_POLICY != 1
+#error "REDSET_STORE_POLICY: 0 (default) or 1 (nt)"
 #endif
 #ifndef REDSET_LOAD_POLICY
 #define REDSET_LOAD_POLICY 1
@@ -260,14 +266,6 @@ __device__ __forceinline__ void load_vec(v4u (&x)[NIN], g_cu4* const (&in)[NIN],
 __device__ __forceinline__ void store_vec(g_u4* p, size_t v, v4u r) {
 #if REDSET_STORE_POLICY == 1
   __builtin_nontemporal_store(r, p + v);
-#elif REDSET_STORE_POLICY == 2
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1 nt" ::"v"(p + v), "v"(r) : "memory");
-#elif REDSET_STORE_POLICY == 3
-  asm volatile("global_store_dwordx4 %0, %1, off sc1 nt" ::"v"(p + v), "v"(r) : "memory");
-#elif REDSET_STORE_POLICY == 4
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 nt" ::"v"(p + v), "v"(r) : "memory");
-#elif REDSET_STORE_POLICY == 5
-  asm volatile("global_store_dwordx4 %0, %1, off sc0 sc1" ::"v"(p + v), "v"(r) : "memory");
 #else
   p[v] = r;
 #endif

@@ -636,7 +636,7 @@ __device__ __forceinline__ void ring_wait_vm() {
 // only the rare fallback pays.
 __device__ __forceinline__ v4u ring_direct_load(g_cu4* p) {
   v4u r;
-  asm volatile("global_load_dwordx4 %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=v"(r) : "v"(p) : "memory");
+  asm volatile("global_load_dwordx4 %0, %1, off nt\n\ts_waitcnt vmcnt(0)" : "=&v"(r) : "v"(p) : "memory");
   return r;
 }
 

@@ -26,6 +26,8 @@
 
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "codec_kernels.h"
 
 // 0 (default): plain sweep -- load a position of every input, wait,
@@ -368,6 +370,71 @@ __device__ __forceinline__ void xor_vec(const v4u (&x)[NIN], g_u4* out, size_t v
   }
 }
 
+// Incremental forms of gf_mac_vec / xor_vec for the loader ring's consumers
+// (ring_sweep): begin(), then add<I0>(x) for inputs [I0, I0 + N) of one
+// 16-B position, then finish(v) stores it. A consumer of a wide stripe adds
+// its inputs in chunks so that only one chunk is live in VGPRs.
+template <int NOUT, bool ACC>
+struct GfAcc {
+  const uint32_t* lds;
+  g_u4* out[NOUT];
+#if REDSET_MEMONLY
+  v4u m;  // timing-only build: XOR instead of GF products (wrong by design)
+  __device__ __forceinline__ void begin() { m = v4u{0, 0, 0, 0}; }
+  template <int I0, int N>
+  __device__ __forceinline__ void add(const v4u (&x)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) m ^= x[i];
+  }
+  __device__ __forceinline__ void finish(size_t v) {
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) {
+      if constexpr (ACC) out[j][v] = m ^ out[j][v];
+      else store_vec(out[j], v, m + j);
+    }
+  }
+#else
+  uint32_t acc[16];
+  __device__ __forceinline__ void begin() {
+#pragma unroll
+    for (int b = 0; b < 16; ++b) acc[b] = 0;
+  }
+  template <int I0, int N>
+  __device__ __forceinline__ void add(const v4u (&x)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) gf_acc_input<sdwa_parts(NOUT)>(lds, x[i], I0 + i, acc);
+  }
+  __device__ __forceinline__ void finish(size_t v) {
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) {
+      v4u r;
+      r.x = gather_byte(acc[0], acc[1], acc[2], acc[3], j);
+      r.y = gather_byte(acc[4], acc[5], acc[6], acc[7], j);
+      r.z = gather_byte(acc[8], acc[9], acc[10], acc[11], j);
+      r.w = gather_byte(acc[12], acc[13], acc[14], acc[15], j);
+      if constexpr (ACC) out[j][v] = r ^ out[j][v];
+      else store_vec(out[j], v, r);
+    }
+  }
+#endif
+};
+
+template <bool ACC>
+struct XorAcc {
+  g_u4* out;
+  v4u r;
+  __device__ __forceinline__ void begin() { r = v4u{0, 0, 0, 0}; }
+  template <int I0, int N>
+  __device__ __forceinline__ void add(const v4u (&x)[N]) {
+#pragma unroll
+    for (int i = 0; i < N; ++i) r ^= x[i];
+  }
+  __device__ __forceinline__ void finish(size_t v) {
+    if constexpr (ACC) out[v] = r ^ out[v];
+    else store_vec(out, v, r);
+  }
+};
+
 // The vector sweep shared by gf_mac and xor_reduce. The job's blocks sweep
 // its cells together, block-interleaved: at any moment they cover one
 // contiguous window of every cell, which keeps HBM row locality across the
@@ -620,6 +687,12 @@ constexpr int ring_slots() {
 #define REDSET_RING_SPIN_CAP (1u << 24)
 #endif
 constexpr unsigned kRingSpinCap = REDSET_RING_SPIN_CAP;
+// Inputs a ring consumer holds in VGPRs at once; wider stripes are combined in
+// two chunks (ring_sweep). A/B knob.
+#ifndef REDSET_RING_CHUNK
+#define REDSET_RING_CHUNK 8
+#endif
+constexpr int kRingChunk = REDSET_RING_CHUNK;
 typedef __attribute__((address_space(3))) v4u lr_u4;
 typedef __attribute__((address_space(3))) volatile unsigned lr_flag;  // LDS, never flat
 __device__ __forceinline__ unsigned ring_flag_ld(unsigned* p) { return *(lr_flag*) p; }
@@ -640,8 +713,9 @@ __device__ __forceinline__ v4u ring_direct_load(g_cu4* p) {
   return r;
 }
 
-// Item k of this block covers vectors (k * G + part) * 64 + lane; `body(x, v)`
-// combines and stores one in-range vector position.
+// Item k of this block covers vectors (k * G + part) * 64 + lane; `body`
+// (GfAcc / XorAcc: begin, add<I0>(inputs), finish(v)) combines and stores one
+// in-range vector position.
 // LDS the ring of a kernel with NIN inputs and R-row items occupies (v4u)
 template <int NIN, int R>
 constexpr int ring_vecs() {
@@ -652,7 +726,7 @@ constexpr int ring_vecs() {
 // caller (gf_mac puts its GF tables in front of it, see gf_mac_body).
 template <int NIN, int R, int D, typename Body>
 __device__ __forceinline__ void ring_sweep(v4u* ring, g_cu4* const (&in)[NIN], size_t nvec, size_t G, size_t part,
-                                           unsigned* fault, Body body) {
+                                           unsigned* fault, Body& body) {
   constexpr int S = ring_slots<NIN * R>();
   static_assert(D >= 1 && D - 1 < S && (D - 1) * NIN * R <= 63, "ring depth");
   constexpr int C = kBlock / 64 - 1;
@@ -741,16 +815,7 @@ __device__ __forceinline__ void ring_sweep(v4u* ring, g_cu4* const (&in)[NIN], s
       }
       __builtin_amdgcn_s_sleep(REDSET_RING_SLEEP);
     }
-    v4u x[R][NIN];
-    if (!direct) {
-      const lr_u4* sl = (const lr_u4*) ring + (k % S) * NIN * R * 64;
-#pragma unroll
-      for (int r = 0; r < R; ++r)
-#pragma unroll
-        for (int i = 0; i < NIN; ++i) x[r][i] = sl[(i * R + r) * 64 + lane];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      if (lane == 0) ring_flag_st(&freed[k % S], want);
-    } else {
+    if (direct) {
       // the item never arrived in time (or the loader stopped): take this
       // lane's bytes from HBM; the ring copy, if it ever lands, is unread.
       // Release the slot for item k + S only after item k - S's consumer
@@ -761,18 +826,63 @@ __device__ __forceinline__ void ring_sweep(v4u* ring, g_cu4* const (&in)[NIN], s
       unsigned s2 = 0;
       while (ring_flag_ld(&freed[k % S]) + 1u < want && ++s2 < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
       if (lane == 0 && ring_flag_ld(&freed[k % S]) + 1u >= want) ring_flag_st(&freed[k % S], want);
+    }
+    const lr_u4* sl = (const lr_u4*) ring + (k % S) * NIN * R * 64;
+    // inputs [I0, I0 + N) of row r into x, from the slot or from HBM
+    auto fetch = [&](auto i0, auto& x, int r) {
+      constexpr int I0 = decltype(i0)::value;
+      constexpr int N = sizeof(x) / sizeof(x[0]);
+      if (!direct) {
 #pragma unroll
-      for (int r = 0; r < R; ++r) {
+        for (int i = 0; i < N; ++i) x[i] = sl[((I0 + i) * R + r) * 64 + lane];
+      } else {
         const size_t v = vec_of(k, r);
         const size_t vc = v < nvec ? v : nvec - 1;
 #pragma unroll
-        for (int i = 0; i < NIN; ++i) x[r][i] = ring_direct_load(in[i] + vc);
+        for (int i = 0; i < N; ++i) x[i] = ring_direct_load(in[I0 + i] + vc);
       }
-    }
+    };
+    auto release = [&]() {
+      if (!direct) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) ring_flag_st(&freed[k % S], want);
+      }
+    };
+    if constexpr (NIN <= kRingChunk) {
+      // the whole item in VGPRs: the slot is free before the arithmetic
+      v4u x[R][NIN];
 #pragma unroll
-    for (int r = 0; r < R; ++r) {
-      const size_t v = vec_of(k, r);
-      if (v < nvec) body(x[r], v);
+      for (int r = 0; r < R; ++r) fetch(std::integral_constant<int, 0>{}, x[r], r);
+      release();
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const size_t v = vec_of(k, r);
+        if (v < nvec) {
+          body.begin();
+          body.template add<0>(x[r]);
+          body.finish(v);
+        }
+      }
+    } else {
+      // wide stripe: two chunks, so only one is live in VGPRs (all NIN inputs
+      // plus the accumulators would spill past the 128 VGPRs of a 1024-thread
+      // block); the slot is held while the first chunk is combined
+      static_assert(R == 1, "wide stripes use one-row items");
+      body.begin();
+      {
+        v4u x[kRingChunk];
+        fetch(std::integral_constant<int, 0>{}, x, 0);
+        body.template add<0>(x);
+      }
+      __builtin_amdgcn_sched_barrier(0);  // keep chunk 1's reads behind chunk 0's arithmetic
+      {
+        v4u x[NIN - kRingChunk];
+        fetch(std::integral_constant<int, kRingChunk>{}, x, 0);
+        release();
+        body.template add<kRingChunk>(x);
+      }
+      const size_t v = vec_of(k, 0);
+      if (v < nvec) body.finish(v);
     }
   }
 }
@@ -807,9 +917,12 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) out[j] = (g_u4*) (J.out[j]);
 #if REDSET_RING
-    ring_sweep<NIN, REDSET_RING_GF_ROWS, REDSET_RING>(
-        smem + kTableVecs, in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
-        [&](const v4u (&x)[NIN], size_t v) { gf_mac_vec<NIN, NOUT, ACC>(lds, x, out, v, true); });
+    GfAcc<NOUT, ACC> body;
+    body.lds = lds;
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) body.out[j] = out[j];
+    ring_sweep<NIN, REDSET_RING_GF_ROWS, REDSET_RING>(smem + kTableVecs, in, nvec, static_cast<size_t>(L.blocks_per_job),
+                                                      static_cast<size_t>(part), L.fault, body);
 #elif REDSET_GLDS
     __shared__ v4u ring_mem[glds_stages<NIN>() * NIN * 64 * kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
@@ -864,9 +977,10 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
     constexpr int kRows = NIN > REDSET_RING_XOR_WIDE ? 1 : REDSET_RING_XOR_ROWS;
     constexpr int kDepth = NIN > REDSET_RING_XOR_WIDE ? REDSET_RING : REDSET_RING_XOR_DEPTH;
     __shared__ v4u ring[ring_vecs<NIN, kRows>()];
-    ring_sweep<NIN, kRows, kDepth>(
-        ring, in, nvec, static_cast<size_t>(L.blocks_per_job), static_cast<size_t>(part), L.fault,
-        [&](const v4u (&x)[NIN], size_t v) { xor_vec<NIN, ACC>(x, out, v, true); });
+    XorAcc<ACC> body;
+    body.out = out;
+    ring_sweep<NIN, kRows, kDepth>(ring, in, nvec, static_cast<size_t>(L.blocks_per_job),
+                                   static_cast<size_t>(part), L.fault, body);
 #else
     sweep<NIN, sweep_prio(3)>(
         in, nvec, vstep, part, [&](const v4u (&x)[NIN], size_t v, bool st) { xor_vec<NIN, ACC>(x, out, v, st); },

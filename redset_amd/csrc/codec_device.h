@@ -693,6 +693,10 @@ constexpr unsigned kRingSpinCap = REDSET_RING_SPIN_CAP;
 #define REDSET_RING_CHUNK 8
 #endif
 constexpr int kRingChunk = REDSET_RING_CHUNK;
+// items in flight for GF kernels with more than kRingChunk inputs (A/B knob)
+#ifndef REDSET_RING_WIDE_DEPTH
+#define REDSET_RING_WIDE_DEPTH REDSET_RING
+#endif
 typedef __attribute__((address_space(3))) v4u lr_u4;
 typedef __attribute__((address_space(3))) volatile unsigned lr_flag;  // LDS, never flat
 __device__ __forceinline__ unsigned ring_flag_ld(unsigned* p) { return *(lr_flag*) p; }
@@ -921,8 +925,9 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
     body.lds = lds;
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) body.out[j] = out[j];
-    ring_sweep<NIN, REDSET_RING_GF_ROWS, REDSET_RING>(smem + kTableVecs, in, nvec, static_cast<size_t>(L.blocks_per_job),
-                                                      static_cast<size_t>(part), L.fault, body);
+    constexpr int kDepth = NIN > kRingChunk ? REDSET_RING_WIDE_DEPTH : REDSET_RING;
+    ring_sweep<NIN, REDSET_RING_GF_ROWS, kDepth>(smem + kTableVecs, in, nvec, static_cast<size_t>(L.blocks_per_job),
+                                                 static_cast<size_t>(part), L.fault, body);
 #elif REDSET_GLDS
     __shared__ v4u ring_mem[glds_stages<NIN>() * NIN * 64 * kWavesPerBlock];
     const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);

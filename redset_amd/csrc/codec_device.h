@@ -646,17 +646,26 @@ __device__ __forceinline__ void gf_mac_glds_sweep(const uint32_t* tables, l_u4* 
 #endif
 constexpr int kRingBudget = REDSET_RING_KIB * 1024;
 // Ring shape per kernel: R = 64-vector rows of every input per item, D =
-// items the loader keeps in flight. gf_mac: 1 row, D = REDSET_RING (the
+// items the loader keeps in flight (ring_depth below). gf_mac: 1 row (the
 // consumers' GF math sets part of the pace; two-row items cost 3%). XOR: 2
-// rows, D = 2 (+3-4% over 1 row, D = 3; profiles/r02_ab_ring_rows.txt).
+// rows (+3-4% over 1 row; profiles/r02_ab_ring_rows.txt).
 #ifndef REDSET_RING_GF_ROWS
 #define REDSET_RING_GF_ROWS 1
 #endif
 #ifndef REDSET_RING_XOR_ROWS
 #define REDSET_RING_XOR_ROWS 2
 #endif
-#ifndef REDSET_RING_XOR_DEPTH
-#define REDSET_RING_XOR_DEPTH 2
+// D is picked so that about REDSET_RING_ROWS_IN_FLIGHT 1 KiB rows are pending
+// behind the item being published: D - 1 = round(16 / (NIN * R)). The rule
+// fits every measured optimum -- RS(8+3): 8 inputs, D = 3; XOR p = 8: 7
+// inputs x 2 rows, D = 2; 16 inputs, D = 2 -- and sets the narrow stripes'
+// depths: 2 inputs +22%, 4 inputs +14%, 6 inputs +2-6% over D = 3
+// (profiles/r03_ring_depth_sweep.txt). REDSET_RING_FIXED_DEPTH > 0 overrides.
+#ifndef REDSET_RING_ROWS_IN_FLIGHT
+#define REDSET_RING_ROWS_IN_FLIGHT 16
+#endif
+#ifndef REDSET_RING_FIXED_DEPTH
+#define REDSET_RING_FIXED_DEPTH 0
 #endif
 // XOR kernels with more inputs than this use the one-row GF shape (A/B knob)
 #ifndef REDSET_RING_XOR_WIDE
@@ -693,10 +702,17 @@ constexpr unsigned kRingSpinCap = REDSET_RING_SPIN_CAP;
 #define REDSET_RING_CHUNK 8
 #endif
 constexpr int kRingChunk = REDSET_RING_CHUNK;
-// items in flight for GF kernels with more than kRingChunk inputs (A/B knob)
-#ifndef REDSET_RING_WIDE_DEPTH
-#define REDSET_RING_WIDE_DEPTH REDSET_RING
-#endif
+// items the loader keeps in flight for NIN inputs of R-row items (see
+// REDSET_RING_ROWS_IN_FLIGHT), within the ring's slots and vmcnt's 6 bits
+template <int NIN, int R>
+constexpr int ring_depth() {
+  constexpr int rows = NIN * R;
+  int d = REDSET_RING_FIXED_DEPTH > 0 ? REDSET_RING_FIXED_DEPTH
+                                      : 1 + (REDSET_RING_ROWS_IN_FLIGHT + rows / 2) / rows;
+  if (d > ring_slots<rows>()) d = ring_slots<rows>();
+  while (d > 1 && (d - 1) * rows > 63) --d;
+  return d < 2 ? 2 : d;
+}
 typedef __attribute__((address_space(3))) v4u lr_u4;
 typedef __attribute__((address_space(3))) volatile unsigned lr_flag;  // LDS, never flat
 __device__ __forceinline__ unsigned ring_flag_ld(unsigned* p) { return *(lr_flag*) p; }
@@ -925,7 +941,7 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
     body.lds = lds;
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) body.out[j] = out[j];
-    constexpr int kDepth = NIN > kRingChunk ? REDSET_RING_WIDE_DEPTH : REDSET_RING;
+    constexpr int kDepth = ring_depth<NIN, REDSET_RING_GF_ROWS>();
     ring_sweep<NIN, REDSET_RING_GF_ROWS, kDepth>(smem + kTableVecs, in, nvec, static_cast<size_t>(L.blocks_per_job),
                                                  static_cast<size_t>(part), L.fault, body);
 #elif REDSET_GLDS
@@ -980,7 +996,7 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
     // no longer fits 1024-thread blocks' 128 VGPRs, so wide XOR sets take
     // the GF kernels' one-row shape
     constexpr int kRows = NIN > REDSET_RING_XOR_WIDE ? 1 : REDSET_RING_XOR_ROWS;
-    constexpr int kDepth = NIN > REDSET_RING_XOR_WIDE ? REDSET_RING : REDSET_RING_XOR_DEPTH;
+    constexpr int kDepth = ring_depth<NIN, kRows>();
     __shared__ v4u ring[ring_vecs<NIN, kRows>()];
     XorAcc<ACC> body;
     body.out = out;

@@ -81,11 +81,11 @@ int read_ring_faults(unsigned* count, int clear);
 // occupancy of the GF kernel for a given input count (blocks per CU)
 int gf_blocks_per_cu(int nin);
 
-// Sweep of the kernels (codec_device.h): REDSET_RING = D > 0 streams the
-// inputs through a loader-wave LDS-DMA ring with D items in flight
-// (ring_sweep), 0 = the plain per-wave sweep.
+// Sweep of the kernels (codec_device.h): REDSET_RING = 1 streams the
+// inputs through a loader-wave LDS-DMA ring (ring_sweep; items in flight per
+// ring_depth), 0 = the plain per-wave sweep.
 #ifndef REDSET_RING
-#define REDSET_RING 3
+#define REDSET_RING 1
 #endif
 // Threads per block, one block per CU: the ring runs 1 loader + 15 consumer
 // waves (1024), the plain sweep 8 waves (512). A/B in profiles/r02_ab_ring.txt,

@@ -655,14 +655,23 @@ constexpr int kRingBudget = REDSET_RING_KIB * 1024;
 #ifndef REDSET_RING_XOR_ROWS
 #define REDSET_RING_XOR_ROWS 2
 #endif
-// D is picked so that about REDSET_RING_ROWS_IN_FLIGHT 1 KiB rows are pending
-// behind the item being published: D - 1 = round(16 / (NIN * R)). The rule
-// fits every measured optimum -- RS(8+3): 8 inputs, D = 3; XOR p = 8: 7
-// inputs x 2 rows, D = 2; 16 inputs, D = 2 -- and sets the narrow stripes'
-// depths: 2 inputs +22%, 4 inputs +14%, 6 inputs +2-6% over D = 3
-// (profiles/r03_ring_depth_sweep.txt). REDSET_RING_FIXED_DEPTH > 0 overrides.
+// D is picked so that about F 1 KiB rows are pending behind the item being
+// published: D - 1 = round(F / (NIN * R)), at most REDSET_RING_MAX_DEPTH items.
+// F = 16 for gf_mac, 20 for xor (its consumers are lighter). Measured on one
+// box for every width 1-16 against fixed D = 2, 3, 4, 6, 9 (profiles/
+// r03_ring_depth_sweep.txt): the rule is best or within run-to-run noise
+// (~2%) everywhere -- RS(8+3): 8 inputs, D = 3; XOR p = 8: 7 inputs x 2
+// rows, D = 2 -- and gains on narrow stripes against round 2's fixed depths:
+// GF 2 / 4 inputs +37% / +17%, XOR 3 inputs +27%. REDSET_RING_FIXED_DEPTH > 0
+// overrides (A/B).
 #ifndef REDSET_RING_ROWS_IN_FLIGHT
 #define REDSET_RING_ROWS_IN_FLIGHT 16
+#endif
+#ifndef REDSET_RING_XOR_ROWS_IN_FLIGHT
+#define REDSET_RING_XOR_ROWS_IN_FLIGHT 20
+#endif
+#ifndef REDSET_RING_MAX_DEPTH
+#define REDSET_RING_MAX_DEPTH 9
 #endif
 #ifndef REDSET_RING_FIXED_DEPTH
 #define REDSET_RING_FIXED_DEPTH 0
@@ -704,11 +713,11 @@ constexpr unsigned kRingSpinCap = REDSET_RING_SPIN_CAP;
 constexpr int kRingChunk = REDSET_RING_CHUNK;
 // items the loader keeps in flight for NIN inputs of R-row items (see
 // REDSET_RING_ROWS_IN_FLIGHT), within the ring's slots and vmcnt's 6 bits
-template <int NIN, int R>
+template <int NIN, int R, int F>
 constexpr int ring_depth() {
   constexpr int rows = NIN * R;
-  int d = REDSET_RING_FIXED_DEPTH > 0 ? REDSET_RING_FIXED_DEPTH
-                                      : 1 + (REDSET_RING_ROWS_IN_FLIGHT + rows / 2) / rows;
+  int d = REDSET_RING_FIXED_DEPTH > 0 ? REDSET_RING_FIXED_DEPTH : 1 + (F + rows / 2) / rows;
+  if (REDSET_RING_FIXED_DEPTH == 0 && d > REDSET_RING_MAX_DEPTH) d = REDSET_RING_MAX_DEPTH;
   if (d > ring_slots<rows>()) d = ring_slots<rows>();
   while (d > 1 && (d - 1) * rows > 63) --d;
   return d < 2 ? 2 : d;
@@ -941,7 +950,7 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
     body.lds = lds;
 #pragma unroll
     for (int j = 0; j < NOUT; ++j) body.out[j] = out[j];
-    constexpr int kDepth = ring_depth<NIN, REDSET_RING_GF_ROWS>();
+    constexpr int kDepth = ring_depth<NIN, REDSET_RING_GF_ROWS, REDSET_RING_ROWS_IN_FLIGHT>();
     ring_sweep<NIN, REDSET_RING_GF_ROWS, kDepth>(smem + kTableVecs, in, nvec, static_cast<size_t>(L.blocks_per_job),
                                                  static_cast<size_t>(part), L.fault, body);
 #elif REDSET_GLDS
@@ -996,7 +1005,7 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
     // no longer fits 1024-thread blocks' 128 VGPRs, so wide XOR sets take
     // the GF kernels' one-row shape
     constexpr int kRows = NIN > REDSET_RING_XOR_WIDE ? 1 : REDSET_RING_XOR_ROWS;
-    constexpr int kDepth = ring_depth<NIN, kRows>();
+    constexpr int kDepth = ring_depth<NIN, kRows, REDSET_RING_XOR_ROWS_IN_FLIGHT>();
     __shared__ v4u ring[ring_vecs<NIN, kRows>()];
     XorAcc<ACC> body;
     body.out = out;

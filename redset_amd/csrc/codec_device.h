@@ -636,8 +636,11 @@ __device__ __forceinline__ void gf_mac_glds_sweep(const uint32_t* tables, l_u4* 
 // profiles/r02s62_gpu_tests_ring_fault.log, fixed at the top of ring_sweep);
 // a build with -DREDSET_RING_SPIN_CAP=4 drives both fallbacks on every
 // launch and is checked bit for bit (tests/test_gpu_ring_fallback.py).
+// LDS for the ring's slots (the GF tables take 2 KiB more): 144 KiB gives
+// wide stripes a slot more (16 inputs: 9 instead of 8), +0.9% on RS(16+4);
+// stripes of <= 8 inputs keep 16 slots (profiles/r03_ring_depth_sweep.txt)
 #ifndef REDSET_RING_KIB
-#define REDSET_RING_KIB 128
+#define REDSET_RING_KIB 144
 #endif
 // 1: a loader that finds its next slot busy first drains and publishes
 // what it holds (A/B knob; 0 = spin on the slot with its items pending)

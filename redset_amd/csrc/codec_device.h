@@ -660,7 +660,8 @@ constexpr int kRingBudget = REDSET_RING_KIB * 1024;
 #endif
 // D is picked so that about F 1 KiB rows are pending behind the item being
 // published: D - 1 = round(F / (NIN * R)), at most REDSET_RING_MAX_DEPTH items.
-// F = 16 for gf_mac, 20 for xor (its consumers are lighter). Measured on one
+// F = 16, except 20 for the one-row items of xor past 8 inputs (light
+// consumers; with two-row items 16 stays best). Measured on one
 // box for every width 1-16 against fixed D = 2, 3, 4, 6, 9 (profiles/
 // r03_ring_depth_sweep.txt): the rule is best or within run-to-run noise
 // (~2%) everywhere -- RS(8+3): 8 inputs, D = 3; XOR p = 8: 7 inputs x 2
@@ -1008,7 +1009,7 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
     // no longer fits 1024-thread blocks' 128 VGPRs, so wide XOR sets take
     // the GF kernels' one-row shape
     constexpr int kRows = NIN > REDSET_RING_XOR_WIDE ? 1 : REDSET_RING_XOR_ROWS;
-    constexpr int kDepth = ring_depth<NIN, kRows, REDSET_RING_XOR_ROWS_IN_FLIGHT>();
+    constexpr int kDepth = ring_depth<NIN, kRows, kRows == 1 ? REDSET_RING_XOR_ROWS_IN_FLIGHT : REDSET_RING_ROWS_IN_FLIGHT>();
     __shared__ v4u ring[ring_vecs<NIN, kRows>()];
     XorAcc<ACC> body;
     body.out = out;

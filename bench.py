@@ -47,10 +47,10 @@ def parse():
     ap.add_argument("--encoding", type=int, default=3, help="parity cells per stripe e")
     ap.add_argument("--chunk-mib", type=float, default=64.0)
     ap.add_argument("--lost", default="1,2", help="members rebuilt each step")
-    ap.add_argument("--cell-pad-mib", type=float, default=16.0,
-                    help="MiB of padding after every cell in HBM: breaks the 2^26-byte aliasing of 64 MiB "
-                         "cells (+2.0%% with stripes in sequence over three alternating pairs, "
-                         "profiles/r02_ab_cell_pad.txt; +1-10%% before, profiles/r01_cell_placement.txt)")
+    ap.add_argument("--cell-pad-mib", type=float, default=-1.0,
+                    help="MiB of padding after every cell in HBM; -1 (default) = the library's recommended "
+                         "stride (redset_hip_cell_stride: 16 MiB after 64 MiB cells, breaking their 2^26-byte "
+                         "aliasing, +2.0%% with stripes in sequence, profiles/r02_ab_cell_pad.txt)")
     ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port beside (rank 0, N=1)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration (RS; XOR gets half)")
     ap.add_argument("--cpu-chunk-mib", type=float, default=0.0,
@@ -201,6 +201,17 @@ def load_traffic(path, kernel_prefix):
         return None
 
 
+def cell_pad(args, chunk):
+    """Bytes after every cell: --cell-pad-mib, or (-1) what the library's
+    recommended stride adds to the 256-B-aligned chunk (include/redset_hip.h
+    redset_hip_cell_stride), the layout INTEGRATION.md advises."""
+    import redset_amd
+
+    if args.cell_pad_mib >= 0:
+        return int(args.cell_pad_mib * MIB)
+    return redset_amd.cell_stride(chunk) - -(-chunk // 256) * 256
+
+
 def timed(step, steps, warmup, dist_on, before=None):
     """W untimed warmups, then K steps bracketed by barrier + synchronize on
     both sides; returns the max-over-ranks elapsed seconds."""
@@ -324,7 +335,7 @@ def xor_leg(args, chunk, stream):
     import redset_amd
 
     p = 8
-    lay = redset_amd.SetLayout.allocate(p, p - 1, 1, chunk, pad=int(args.cell_pad_mib * MIB))
+    lay = redset_amd.SetLayout.allocate(p, p - 1, 1, chunk, pad=cell_pad(args, chunk))
     g = torch.Generator(device="cuda")
     g.manual_seed(77)
     for r in range(p):
@@ -506,7 +517,7 @@ def main():
 
     # this rank's own set, all cells resident in HBM
     codec = redset_amd.RSCodec(p, e)
-    lay = redset_amd.SetLayout.allocate(p, d, e, chunk, pad=int(args.cell_pad_mib * MIB))
+    lay = redset_amd.SetLayout.allocate(p, d, e, chunk, pad=cell_pad(args, chunk))
     g = torch.Generator(device="cuda")
     g.manual_seed(1234 + rank)
     for r in range(p):

@@ -1044,8 +1044,38 @@ __device__ __forceinline__ int job_block(int b, int per_job) {
 
 // entry points: jobs from a device array (plans), or one job passed by
 // value in the kernel arguments (stripe primitives, no device descriptor)
+// Timing-only knob (never shipped): every block records its start and end
+// (s_memrealtime, 100 MHz) and its hardware placement into the words behind
+// the fault word (codec_kernels.hip sizes them; read by
+// redset_hip_debug_block_clock), to see how evenly a launch's blocks finish.
+#ifndef REDSET_BLOCK_CLOCK
+#define REDSET_BLOCK_CLOCK 0
+#endif
+struct BlockClock {
+#if REDSET_BLOCK_CLOCK
+  unsigned long long t0;
+  unsigned* fault;
+  __device__ __forceinline__ explicit BlockClock(unsigned* f) : t0(__builtin_amdgcn_s_memrealtime()), fault(f) {}
+  __device__ __forceinline__ ~BlockClock() {
+    __syncthreads();
+    if (threadIdx.x == 0 && fault) {
+      unsigned hw, xcc;
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+      asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+      unsigned long long* c = reinterpret_cast<unsigned long long*>(fault + 64) + 3 * blockIdx.x;
+      c[0] = t0;
+      c[1] = __builtin_amdgcn_s_memrealtime();
+      c[2] = (static_cast<unsigned long long>(xcc) << 32) | hw;
+    }
+  }
+#else
+  __device__ __forceinline__ explicit BlockClock(unsigned*) {}
+#endif
+};
+
 template <int NIN, int NOUT, bool ACC>
 REDSET_KERNEL gf_mac_kernel(GfLaunch L) {
+  BlockClock clock(L.fault);
   if (L.sequential == kJobsInKernel) {
     // every block sweeps every job in turn: one stripe's cells in flight at
     // a time, with no launch boundary between stripes
@@ -1066,6 +1096,7 @@ REDSET_KERNEL gf_mac_kernel_arg(GfLaunch L, GfJob J) {
 
 template <int NIN, bool ACC>
 REDSET_KERNEL xor_kernel(XorLaunch L) {
+  BlockClock clock(L.fault);
   if (L.sequential == kJobsInKernel) {
     for (int j = 0; j < L.njobs; ++j) xor_body<NIN, ACC>(L, L.jobs[j], blockIdx.x);
     return;

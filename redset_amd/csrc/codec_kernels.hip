@@ -42,7 +42,14 @@ int jobs_per_launch(const Launch& L) {
 // from several threads (the pipeline's compute thread, per-rank backends,
 // callers), so the per-device address cache is atomic; a racing first
 // lookup resolves the same address twice, which is harmless.
+#if REDSET_BLOCK_CLOCK
+// timing-only builds: the fault word, then 3 words of 64 bits per block
+// (codec_device.h BlockClock)
+constexpr int kClockBlocks = 4096;
+__device__ unsigned g_ring_fault[64 + 6 * kClockBlocks];
+#else
 __device__ unsigned g_ring_fault;
+#endif
 
 unsigned* ring_fault_word() {
   static std::atomic<unsigned*> addr[64];
@@ -70,6 +77,18 @@ int read_ring_faults(unsigned* count, int clear) {
   if (count) *count = v;
   return e;
 }
+
+#if REDSET_BLOCK_CLOCK
+}  // namespace redset_hip
+// timing-only builds: (start, end, XCC_ID << 32 | HW_ID) of blocks [0, n) of
+// the last gf_mac / xor launch
+extern "C" int redset_hip_debug_block_clock(unsigned long long* out, int n) {
+  if (n > redset_hip::kClockBlocks) n = redset_hip::kClockBlocks;
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(redset_hip::g_ring_fault), 3 * sizeof(unsigned long long) * n,
+                             64 * sizeof(unsigned), hipMemcpyDeviceToHost);
+}
+namespace redset_hip {
+#endif
 
 int device_cu_count() {
   static int cus = 0;

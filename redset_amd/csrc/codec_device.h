@@ -772,6 +772,14 @@ __device__ __forceinline__ void ring_sweep(v4u* ring, g_cu4* const (&in)[NIN], s
   if (threadIdx.x < S) full[threadIdx.x] = 0, freed[threadIdx.x] = 0;
   if (threadIdx.x == 0) bypass = 0;
   __syncthreads();
+  // Nothing the compiler knows of may be in flight when the loops start: its
+  // wait insertion merges the state at a loop's entry into the loop, so a
+  // load or store still pending here (job descriptor, tables, a previous
+  // job's stores) whose registers the loader loop reuses puts a vmcnt(0)
+  // into that loop -- every item then waits for all earlier LDS-DMA loads
+  // (the loader's pipelining gone, a launch 60% slower; it happened to an
+  // instrumented build). This wait, which the compiler does see, clears it.
+  __builtin_amdgcn_s_waitcnt(0);
   const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
   const int lane = threadIdx.x & 63;
   const size_t rows = (nvec + 63) / 64;
@@ -1053,20 +1061,34 @@ __device__ __forceinline__ int job_block(int b, int per_job) {
 #endif
 struct BlockClock {
 #if REDSET_BLOCK_CLOCK
-  unsigned long long t0;
-  unsigned* fault;
-  __device__ __forceinline__ explicit BlockClock(unsigned* f) : t0(__builtin_amdgcn_s_memrealtime()), fault(f) {}
-  __device__ __forceinline__ ~BlockClock() {
-    __syncthreads();
-    if (threadIdx.x == 0 && fault) {
+  // block start (thread 64) and every consumer wave's end (atomicMax by its
+  // lane 0): no barrier, and nothing from the ring's loader wave (wave 0) --
+  // a compiler-visible store in that wave makes hipcc put a vmcnt(0) wait
+  // into its LDS-DMA issue loop (measured: the launch 60% slower)
+  unsigned long long* c;
+  __device__ __forceinline__ explicit BlockClock(unsigned* f)
+      : c(reinterpret_cast<unsigned long long*>(f + 64) + 3 * blockIdx.x) {
+    if (threadIdx.x == 64) {
       unsigned hw, xcc;
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
       asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-      unsigned long long* c = reinterpret_cast<unsigned long long*>(fault + 64) + 3 * blockIdx.x;
-      c[0] = t0;
-      c[1] = __builtin_amdgcn_s_memrealtime();
-      c[2] = (static_cast<unsigned long long>(xcc) << 32) | hw;
+      const unsigned long long t = __builtin_amdgcn_s_memrealtime();
+      const unsigned long long id = (static_cast<unsigned long long>(xcc) << 32) | hw;
+      // one asm block, stores and their wait: no VMEM event the compiler's
+      // wait insertion could carry into the loader's loop (a plain store here
+      // does, see above)
+      asm volatile(
+          "global_store_dwordx2 %0, %1, off\n\t"
+          "global_store_dwordx2 %0, %2, off offset:8\n\t"
+          "global_store_dwordx2 %0, %3, off offset:16\n\t"
+          "s_waitcnt vmcnt(0)"
+          :
+          : "v"(c), "v"(t), "v"(0ull), "v"(id)
+          : "memory");
     }
+  }
+  __device__ __forceinline__ ~BlockClock() {
+    if ((threadIdx.x & 63) == 0 && threadIdx.x >= 64) atomicMax(c + 1, __builtin_amdgcn_s_memrealtime());
   }
 #else
   __device__ __forceinline__ explicit BlockClock(unsigned*) {}

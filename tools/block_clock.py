@@ -26,6 +26,7 @@ from redset_amd import _lib  # noqa: E402
 
 MiB = 1 << 20
 TICK_US = 0.01  # s_memrealtime runs at 100 MHz
+CLOCK = False
 
 
 def read_clock(n=4096):
@@ -62,7 +63,23 @@ def summarize(rows):
     }
 
 
-def run(name, plan, reps):
+def event_us(plan, reps, launches):
+    """mean event-timed microseconds per launch of the plan"""
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    plan.execute()
+    a.record()
+    for _ in range(reps):
+        plan.execute()
+    b.record()
+    torch.cuda.synchronize()
+    return round(a.elapsed_time(b) * 1000 / reps / launches, 2)
+
+
+def run(name, plan, reps, launches):
+    ev = event_us(plan, reps, launches)
+    if not CLOCK:
+        print(json.dumps({"case": name, "lib": _lib.LIB_PATH, "event_us_per_launch": ev}), flush=True)
+        return
     plan.execute()
     out = []
     for _ in range(reps):
@@ -70,12 +87,14 @@ def run(name, plan, reps):
         out.append(summarize(read_clock()))
     keys = ("ramp_us", "span_us", "busy_mean_us", "edge_idle_frac")
     mean = {k: round(float(np.mean([o[k] for o in out])), 4) for k in keys}
-    print(json.dumps({"case": name, "mean": mean, "last": out[-1]}), flush=True)
+    print(json.dumps({"case": name, "lib": _lib.LIB_PATH, "event_us_per_launch": ev, "mean": mean,
+                      "last": out[-1]}), flush=True)
 
 
 def main():
     reps = int(sys.argv[1]) if len(sys.argv) > 1 else 10
-    assert hasattr(_lib.load(), "redset_hip_debug_block_clock"), "needs a -DREDSET_BLOCK_CLOCK=1 build"
+    global CLOCK
+    CLOCK = hasattr(_lib.load(), "redset_hip_debug_block_clock")  # else event times only
     C = 64 * MiB
     p, e = 11, 3
     pad = redset_amd.cell_stride(C) - C
@@ -85,8 +104,8 @@ def main():
         lay.lofi(r).random_(0, 256)
     enc = codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), C, lay.cell_stride)
     reb = codec.plan_rebuild([1, 2], lay.lofi_ptrs(), lay.parity_ptrs(), C, lay.cell_stride)
-    run("rs_encode_8_3", enc, reps)
-    run("rs_rebuild_8_2", reb, reps)
+    run("rs_encode_8_3", enc, reps, p)
+    run("rs_rebuild_8_2", reb, reps, p)
     del enc, reb, lay
     torch.cuda.empty_cache()
     px = 8
@@ -94,7 +113,7 @@ def main():
     for r in range(px):
         xl.lofi(r).random_(0, 256)
     xe = redset_amd.xor_plan_encode(px, xl.lofi_ptrs(), xl.parity_ptrs(), C, xl.cell_stride)
-    run("xor_encode_7", xe, reps)
+    run("xor_encode_7", xe, reps, px)
 
 
 if __name__ == "__main__":

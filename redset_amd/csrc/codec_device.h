@@ -275,7 +275,10 @@ __device__ __forceinline__ void store_vec(g_u4* p, size_t v, v4u r) {
 
 // acc (packed partial products of all outputs, 16 bytes) ^= coef[.][i] * x;
 // SDWA: table offsets by SDWA byte selects (see REDSET_SDWA_OFFSETS)
-template <int SDWA>
+// TB: byte offset of the tables in LDS (a constant, so it folds into the
+// ds_read immediate like the input's own offset; the streamed kernels keep
+// two jobs' tables, TB selects one)
+template <int SDWA, int TB = 0>
 __device__ __forceinline__ void gf_acc_input(const uint32_t* lds, const v4u& x, int i, uint32_t (&acc)[16]) {
   const uint32_t w[4] = {x.x, x.y, x.z, x.w};
 #pragma unroll
@@ -306,8 +309,8 @@ __device__ __forceinline__ void gf_acc_input(const uint32_t* lds, const v4u& x, 
     }
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
-      acc[4 * q + b] = xor3(acc[4 * q + b], lds_at(lds, i * kTableBytes + ol[b]),
-                            lds_hi_at(lds, i * kTableBytes + kHiBase + oh[b]));
+      acc[4 * q + b] = xor3(acc[4 * q + b], lds_at(lds, TB + i * kTableBytes + ol[b]),
+                            lds_hi_at(lds, TB + i * kTableBytes + kHiBase + oh[b]));
     }
   }
 }
@@ -381,7 +384,7 @@ struct GfAcc {
 #if REDSET_MEMONLY
   v4u m;  // timing-only build: XOR instead of GF products (wrong by design)
   __device__ __forceinline__ void begin() { m = v4u{0, 0, 0, 0}; }
-  template <int I0, int N>
+  template <int I0, int N, int TB = 0>
   __device__ __forceinline__ void add(const v4u (&x)[N]) {
 #pragma unroll
     for (int i = 0; i < N; ++i) m ^= x[i];
@@ -399,10 +402,10 @@ struct GfAcc {
 #pragma unroll
     for (int b = 0; b < 16; ++b) acc[b] = 0;
   }
-  template <int I0, int N>
+  template <int I0, int N, int TB = 0>
   __device__ __forceinline__ void add(const v4u (&x)[N]) {
 #pragma unroll
-    for (int i = 0; i < N; ++i) gf_acc_input<sdwa_parts(NOUT)>(lds, x[i], I0 + i, acc);
+    for (int i = 0; i < N; ++i) gf_acc_input<sdwa_parts(NOUT), TB>(lds, x[i], I0 + i, acc);
   }
   __device__ __forceinline__ void finish(size_t v) {
 #pragma unroll
@@ -709,6 +712,11 @@ constexpr int ring_slots() {
 #define REDSET_RING_SPIN_CAP (1u << 24)
 #endif
 constexpr unsigned kRingSpinCap = REDSET_RING_SPIN_CAP;
+// Waits that end by construction and have no fallback (the streamed kernels'
+// table hand-over and a position's claim): their cap is only insurance
+// against a hang from a bug, counted like a capped spin, and independent of
+// the test knob above (a capped table wait would use another job's tables).
+constexpr unsigned kRingHangCap = 1u << 26;
 // Inputs a ring consumer holds in VGPRs at once; wider stripes are combined in
 // two chunks (ring_sweep). A/B knob.
 #ifndef REDSET_RING_CHUNK
@@ -929,20 +937,28 @@ __device__ __forceinline__ void ring_sweep(v4u* ring, g_cu4* const (&in)[NIN], s
 }
 #endif
 
-template <int NIN, int NOUT, bool ACC>
-__device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, int part) {
-  // One static LDS array, the GF tables first and the loader ring behind
-  // them: the tables' addresses (< 2 KiB) then fold into ds_read's 16-bit
-  // immediate offset, so a lookup's address is the table offset alone. As two
-  // arrays the compiler put the 128 KiB ring first, and every lookup paid a
-  // v_add of the tables' base (0x20000) -- 4 of ~20 VALU ops per input dword.
-  constexpr int kTableVecs = kMaxIn * kTableBytes / 16;
+// One static LDS array per input count, the GF tables first and the loader
+// ring behind them: the tables' addresses (< 2 KiB) then fold into ds_read's
+// 16-bit immediate offset, so a lookup's address is the table offset alone. As
+// two arrays the compiler put the 128 KiB ring first, and every lookup paid a
+// v_add of the tables' base (0x20000) -- 4 of ~20 VALU ops per input dword.
+// (A function-scope static: gf_mac_body and gf_mac_stream share it, where two
+// arrays would each get their own LDS.)
+constexpr int kTableVecs = kMaxIn * kTableBytes / 16;
+template <int NIN>
+__device__ __forceinline__ v4u* gf_lds() {
 #if REDSET_RING
   constexpr int kRingVecs = ring_vecs<NIN, REDSET_RING_GF_ROWS>();
 #else
   constexpr int kRingVecs = 0;
 #endif
   __shared__ v4u smem[kTableVecs + kRingVecs];
+  return smem;
+}
+
+template <int NIN, int NOUT, bool ACC>
+__device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, int part) {
+  v4u* const smem = gf_lds<NIN>();
   uint32_t* const lds = reinterpret_cast<uint32_t*>(smem);
 
   build_tables(lds, J, NIN, NOUT);
@@ -1002,6 +1018,655 @@ __device__ __forceinline__ void gf_mac_body(const GfLaunch& L, const GfJob& J, i
     }
   }
 }
+
+#if REDSET_RING
+// kJobsStreamed (codec_kernels.h): one launch, every block streams its items
+// of ALL the launch's jobs (stripes) through one continuous loader ring --
+// job 0's items, then job 1's, ... -- so a block that finishes its share of
+// a stripe goes straight on to the next stripe's: no launch gap and no
+// per-stripe tail (the edges of a launch idle 3.5% of its CU time and
+// launches sit 2.5 us apart, profiles/r03_block_clock.txt), and no ring
+// drain between stripes. The GF tables of two jobs live in the table region
+// (NIN <= 8: 2 x NIN x 128 B <= 2 KiB), job j's in buffer j & 1; the loader
+// wave builds job j's tables when it reaches job j's first item, once every
+// consumer is past job j - 2's items (prog[], the next item each consumer
+// takes), and announces them in tab_job. Consumers pick the buffer by a
+// branch over two copies of the arithmetic, so the tables' offsets still
+// fold into the ds_read immediates. Deadlock freedom: a consumer waits only
+// on FULL (capped: direct loads) and on tab_job; the loader's wait on prog
+// needs only items of jobs <= j - 2, whose tables exist, so it always ends.
+// Same staging rules as ring_sweep (capped FULL/FREE waits, BYPASS).
+// Host side: only for whole 16-B vectors (!bytes_only, nbytes % 16 == 0)
+// and NIN <= 8 (redset_hip.cpp).
+template <int NIN, int NOUT>
+__device__ __forceinline__ void build_tables_wave(uint32_t* lds, int tb, const __attribute__((address_space(4))) GfJob* J,
+                                                  int lane) {
+  // lanes 0-31: input i2, lanes 32-63: input i2 + 1; lane & 31 = (half, nibble);
+  // the coefficients are wave-uniform (scalar loads, nothing on vmcnt)
+  const int h = (lane >> 4) & 1;
+  const int n = lane & 15;
+  const uint32_t x = static_cast<uint32_t>(n) << (4 * h);
+  // coefficient rows as dwords: byte loads would be vector loads, whose waits
+  // (vmcnt) would also drain the loader's LDS-DMA queue
+  typedef __attribute__((address_space(4))) const uint32_t c_u32;
+  uint32_t cw[NOUT][(NIN + 3) / 4];
+#pragma unroll
+  for (int j = 0; j < NOUT; ++j)
+#pragma unroll
+    for (int q = 0; q < (NIN + 3) / 4; ++q) cw[j][q] = ((c_u32*) &J->coef[j][0])[q];
+  auto coef = [&](int j, int i) { return (cw[j][i >> 2] >> (8 * (i & 3))) & 0xFFu; };
+#pragma unroll
+  for (int i2 = 0; i2 < NIN; i2 += 2) {
+    const int i = i2 + (lane >> 5);
+    if (i < NIN) {
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < NOUT; ++j) {
+        const uint32_t c0 = coef(j, i2);
+        const uint32_t c1 = (i2 + 1 < NIN) ? coef(j, i2 + 1) : 0u;
+        v |= gf_mul_dev((lane >> 5) ? c1 : c0, x) << (8 * j);
+      }
+      const int off = tb + i * kTableBytes + (h ? kHiBase + n * kHiStride : n * 4);
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<char*>(lds) + off) = v;
+    }
+  }
+}
+
+template <int NIN, int NOUT, bool ACC>
+__device__ __forceinline__ void gf_mac_stream(const GfLaunch& L) {
+  static_assert(NIN <= 8 && 2 * NIN * kTableBytes <= kTableVecs * 16, "two jobs' tables in the table region");
+  static_assert(REDSET_RING_GF_ROWS == 1, "one-row items");
+  constexpr int S = ring_slots<NIN>();
+  constexpr int D = ring_depth<NIN, 1, REDSET_RING_ROWS_IN_FLIGHT>();
+  constexpr int C = kBlock / 64 - 1;
+  constexpr int kTab = NIN * kTableBytes;  // one job's tables (bytes)
+  static_assert(D >= 2 && D - 1 < S && (D - 1) * NIN <= 63, "ring depth");
+  typedef __attribute__((address_space(4))) const GfJob c_job;
+  const c_job* const jobs = (const c_job*) (L.jobs + L.job0);
+  v4u* const smem = gf_lds<NIN>();
+  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem);
+  v4u* const ring = smem + kTableVecs;
+  __shared__ unsigned full[S], freed[S], bypass, tab_job, prog[C];
+
+  const size_t nvec = L.nbytes / 16;
+  const size_t G = gridDim.x;
+  const size_t part = blockIdx.x;
+  const size_t rows = (nvec + 63) / 64;
+  const unsigned K = rows > part ? static_cast<unsigned>((rows - part + G - 1) / G) : 0u;
+  const unsigned njobs = static_cast<unsigned>(L.njobs);
+  const unsigned total = K * njobs;
+  if (K == 0) return;  // uniform over the block: no work here
+
+  // job 0's tables into buffer 0 (the whole block), flags
+  for (int e = threadIdx.x; e < NIN * 32; e += blockDim.x) {
+    const int i = e >> 5, h = (e >> 4) & 1, n = e & 15;
+    const uint32_t x = static_cast<uint32_t>(n) << (4 * h);
+    uint32_t v = 0;
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) v |= gf_mul_dev(jobs[0].coef[j][i], x) << (8 * j);
+    lds[(i * kTableBytes + (h ? kHiBase + n * kHiStride : n * 4)) / 4] = v;
+  }
+  if (threadIdx.x < S) full[threadIdx.x] = 0, freed[threadIdx.x] = 0;
+  if (threadIdx.x < C) prog[threadIdx.x] = threadIdx.x;
+  if (threadIdx.x == 0) bypass = 0, tab_job = 0;
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);  // see ring_sweep
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  auto vec_of = [&](unsigned k) { return (static_cast<size_t>(k) * G + part) * 64 + lane; };
+
+  if (wave == 0) {
+    if constexpr (REDSET_RING_LOADER_PRIO > 0) __builtin_amdgcn_s_setprio(REDSET_RING_LOADER_PRIO);
+    const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lr_u4*) ring)));
+    unsigned pub = 0;  // items [pub, g) are issued and not yet published
+    auto publish = [&]() {
+      if (lane == 0) ring_flag_st(&full[pub % S], pub / S + 1);
+      ++pub;
+    };
+    // every consumer's next item is >= T (all items before T are done)
+    auto past = [&](unsigned T) {
+      const bool ok = lane >= C || ring_flag_ld(&prog[lane]) >= T;
+      return __builtin_amdgcn_ballot_w64(!ok) == 0;
+    };
+    // job j's tables into buffer j & 1, once every consumer is past job
+    // j - 2; if they are not yet, first publish every item issued (with
+    // fewer items per job than in flight, some may be job j - 2's)
+    auto next_tables = [&](unsigned j, unsigned g) {
+      if (j >= 2 && !past((j - 1) * K)) {
+        ring_wait_vm<0>();
+        while (pub < g) publish();
+        // always ends (see above); the cap only keeps a bug from hanging the
+        // GPU -- a capped wait is counted and every test checks the count
+        unsigned spins = 0;
+        while (!past((j - 1) * K) && ++spins < kRingHangCap) __builtin_amdgcn_s_sleep(1);
+        if (spins >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+      }
+      build_tables_wave<NIN, NOUT>(lds, (j & 1) * kTab, jobs + j, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) ring_flag_st(&tab_job, j);
+    };
+    const uint8_t* in[NIN];
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) in[i] = jobs[0].in[i];
+    unsigned job = 0, k = 0;
+    for (unsigned g = 0; g < total; ++g, ++k) {
+      if (k == K) {
+        k = 0;
+        ++job;
+        next_tables(job, g);
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) in[i] = jobs[job].in[i];
+      }
+      const unsigned use = g / S;
+      if (ring_flag_ld(&freed[g % S]) < use) {
+#if REDSET_RING_DRAIN
+        ring_wait_vm<0>();
+        while (pub < g) publish();
+#endif
+        unsigned spins = 0;
+        while (ring_flag_ld(&freed[g % S]) < use && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+        if (spins >= kRingSpinCap) {
+          // as in ring_sweep: publish what is issued, hand the rest to the
+          // consumers' direct loads -- but keep building the tables they need
+          ring_wait_vm<0>();
+          while (pub < g) publish();
+          if (lane == 0) {
+            ring_flag_st(&bypass, 1u);
+            if (L.fault) atomicAdd(L.fault, 1u);
+          }
+          for (unsigned j = job + 1; j < njobs; ++j) next_tables(j, g);
+          return;
+        }
+      }
+      const uint32_t slot = ring0 + (g % S) * NIN * 1024;
+      const size_t v = vec_of(k);
+      const size_t vc = v < nvec ? v : nvec - 1;
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) {
+        uint32_t keep;
+        asm volatile(
+            "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+#if REDSET_LOAD_POLICY == 1
+            " nt"
+#endif
+            "\n\ts_mov_b32 m0, %0"
+            : "=&s"(keep)
+            : "v"((g_cu4*) (in[i]) + vc), "s"(slot + static_cast<uint32_t>(i * 1024))
+            : "memory");
+      }
+      if (g + 1 - pub == static_cast<unsigned>(D)) {
+        ring_wait_vm<(D - 1) * NIN>();
+        publish();
+      }
+    }
+    ring_wait_vm<0>();
+    while (pub < total) publish();
+    return;
+  }
+
+  // consumers: items c, c + C, ... of the block's sequence
+  const int c = wave - 1;
+  GfAcc<NOUT, ACC> body;
+  body.lds = lds;
+  g_cu4* in[NIN];
+  int cur = -1;
+  unsigned job = static_cast<unsigned>(c) / K, k = static_cast<unsigned>(c) % K;
+  for (unsigned g = c; g < total; g += C) {
+    if (static_cast<int>(job) != cur) {
+      cur = static_cast<int>(job);
+      unsigned spins = 0;  // always ends; capped as the loader's wait above
+      while (ring_flag_ld(&tab_job) < job && ++spins < kRingHangCap) __builtin_amdgcn_s_sleep(REDSET_RING_SLEEP);
+      if (spins >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (jobs[job].in[i]);
+#pragma unroll
+      for (int j = 0; j < NOUT; ++j) body.out[j] = (g_u4*) (jobs[job].out[j]);
+    }
+    const unsigned want = g / S + 1;
+    unsigned spins = 0;
+    bool direct = false;
+    while (ring_flag_ld(&full[g % S]) < want) {
+      if (ring_flag_ld(&bypass) != 0u || ++spins >= kRingSpinCap) {
+        direct = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(REDSET_RING_SLEEP);
+    }
+    const size_t v = vec_of(k);
+    v4u x[NIN];
+    if (!direct) {
+      const lr_u4* sl = (const lr_u4*) ring + (g % S) * NIN * 64;
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) x[i] = sl[i * 64 + lane];
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) ring_flag_st(&freed[g % S], want);
+    } else {
+      // as in ring_sweep
+      if (spins >= kRingSpinCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+      unsigned s2 = 0;
+      while (ring_flag_ld(&freed[g % S]) + 1u < want && ++s2 < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+      if (lane == 0 && ring_flag_ld(&freed[g % S]) + 1u >= want) ring_flag_st(&freed[g % S], want);
+      const size_t vc = v < nvec ? v : nvec - 1;
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) x[i] = ring_direct_load(in[i] + vc);
+    }
+    if (v < nvec) {
+      body.begin();
+      if (job & 1) body.template add<0, NIN, kTab>(x);
+      else body.template add<0, NIN, 0>(x);
+      body.finish(v);
+    }
+    // this item's lookups are done (finish used their results): its job's
+    // table buffer may be rebuilt once every consumer says so
+    if (lane == 0) ring_flag_st(&prog[c], g + C);
+    k += C;
+    while (k >= K) k -= K, ++job;
+  }
+  if (lane == 0) ring_flag_st(&prog[c], 0xFFFFFFFFu);
+}
+#endif
+
+#if REDSET_RING
+// Slow, table-free product of one 16-B position (the claimed kernel's last
+// resort, for items whose tables may not exist: see gf_mac_claimed): a dword
+// at a time, bytes multiplied in parallel within it (shift-and-add with the
+// 0x11D reduction per byte), loops kept rolled so that it adds few registers
+// to the consumer loop it sits in
+__device__ __forceinline__ uint32_t gf_mul_bytes(uint32_t c, uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll 1
+  for (int b = 0; b < 8; ++b) {
+    if ((c >> b) & 1u) r ^= x;
+    x = ((x & 0x7F7F7F7Fu) << 1) ^ (((x >> 7) & 0x01010101u) * 0x1Du);
+  }
+  return r;
+}
+template <int NIN, int NOUT, bool ACC>
+__device__ __forceinline__ void gf_mac_vec_slow(const __attribute__((address_space(4))) GfJob* J, g_cu4* const (&in)[NIN],
+                                                size_t v) {
+#pragma unroll 1
+  for (int j = 0; j < NOUT; ++j) {
+    uint32_t* o = reinterpret_cast<uint32_t*>(J->out[j]) + 4 * v;
+#pragma unroll 1
+    for (int w = 0; w < 4; ++w) {
+      uint32_t r = 0;
+#pragma unroll 1
+      for (int i = 0; i < NIN; ++i)
+        r ^= gf_mul_bytes(J->coef[j][i], reinterpret_cast<const uint32_t*>(J->in[i])[4 * v + w]);
+      o[w] = ACC ? (o[w] ^ r) : r;
+    }
+  }
+}
+
+// items per claim, and batches the claimer keeps claimed ahead of the loader
+#ifndef REDSET_CLAIM_BATCH
+#define REDSET_CLAIM_BATCH 4
+#endif
+#ifndef REDSET_CLAIM_LOOK
+#define REDSET_CLAIM_LOOK 2
+#endif
+// kJobsClaimed: gf_mac_stream's continuous ring over all the launch's jobs,
+// with the items claimed at run time. The rows of every job are dealt to 8
+// queues (row % 8; block b serves queue b % 8, i.e. one queue per XCD, as the
+// static mapping deals rows to XCDs; one queue if the grid is not a multiple
+// of 8); the blocks of a queue claim batches of B consecutive items with a
+// returning atomic on the queue's counter, so they sweep the XCD's rows in
+// order together and finish together: no block runs ahead into the next
+// stripe (gf_mac_stream's drift: all 11 stripes in one launch lost 3.5%,
+// profiles/r03_ab_stream.txt) and none idles at the end of a stripe.
+// Queue item u: job u / RQ, row (u % RQ) * nq + q, RQ = ceil(rows / nq) rounded
+// up to B (a batch never spans two jobs; rows past the end are skipped).
+// Wave 1 is the claimer: it keeps up to kLook batches claimed ahead of the
+// loader (bbase[], nclaimed; its atomic's wait stalls only itself -- in the
+// loader a returning atomic would drain the LDS-DMA queue with vmcnt(0)).
+// Ring position p holds item bbase[(p / B) % NB] + p % B (the loader also
+// records it in pitem[] before publishing). Waves 2-15 consume.
+// Fallbacks (capped waits): a consumer loads an unpublished position straight
+// from HBM, its item from bbase[] (not overwritten before every position of
+// that batch was released: NB * B >= S + (kLook + 1) * B); a capped loader
+// stops (BYPASS), the claimer stops, the consumers finish the claimed
+// batches and then claim batches themselves, computing without tables where
+// the loader never built them (gf_mac_vec_slow). Capped waits are counted.
+// The last block to finish zeroes the counters for the next launch.
+template <int NIN, int NOUT, bool ACC>
+__device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
+  static_assert(NIN <= 8 && 2 * NIN * kTableBytes <= kTableVecs * 16, "two jobs' tables in the table region");
+  static_assert(REDSET_RING_GF_ROWS == 1, "one-row items");
+  constexpr int S = ring_slots<NIN>();
+  constexpr int D = ring_depth<NIN, 1, REDSET_RING_ROWS_IN_FLIGHT>();
+  constexpr int C = kBlock / 64 - 2;  // consumer waves
+  constexpr int kTab = NIN * kTableBytes;
+  constexpr unsigned B = REDSET_CLAIM_BATCH;
+  constexpr unsigned kLook = REDSET_CLAIM_LOOK;
+  constexpr unsigned NB = 32;
+  static_assert(C >= 1 && NB * B >= S + (kLook + 1) * B, "batch ring");
+  typedef __attribute__((address_space(4))) const GfJob c_job;
+  const c_job* const jobs = (const c_job*) (L.jobs + L.job0);
+  v4u* const smem = gf_lds<NIN>();
+  uint32_t* const lds = reinterpret_cast<uint32_t*>(smem);
+  v4u* const ring = smem + kTableVecs;
+  __shared__ unsigned full[S], freed[S], pitem[S], prog[C], bbase[NB];
+  __shared__ unsigned bypass, tab_job, seq_end, nclaimed, claim_end, lbatch, first;
+
+  const size_t nvec = L.nbytes / 16;
+  const unsigned rows = static_cast<unsigned>((nvec + 63) / 64);
+  // queue of this block: blockIdx % 8 (the XCD the dispatcher deals it to);
+  // one queue when the grid is not a multiple of 8 blocks, so that every
+  // queue has blocks and all queues the same number of them
+  const unsigned nq = (gridDim.x % kClaimQueues == 0) ? kClaimQueues : 1u;
+  const unsigned q = blockIdx.x % nq;
+  const unsigned RQ = ((rows + nq - 1) / nq + B - 1) / B * B;
+  const unsigned njobs = static_cast<unsigned>(L.njobs);
+  const unsigned total = RQ * njobs;  // items of one queue
+  unsigned* const qctr = L.claim + q * kClaimStride;
+  unsigned* const fin = L.claim + kClaimQueues * kClaimStride;
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  auto vec_of = [&](unsigned u) { return (static_cast<size_t>((u % RQ) * nq + q)) * 64 + lane; };
+  auto row_ok = [&](unsigned u) { return (u % RQ) * nq + q < rows; };
+
+  if (threadIdx.x == 0) {
+    const unsigned b0 = atomicAdd(qctr, B);
+    bbase[0] = b0;
+    first = b0;
+  }
+  __syncthreads();
+  const unsigned b0 = first;
+  if (b0 < total) {
+    const unsigned job0 = b0 / RQ;
+    for (int e = threadIdx.x; e < NIN * 32; e += blockDim.x) {
+      const int i = e >> 5, h = (e >> 4) & 1, n = e & 15;
+      const uint32_t x = static_cast<uint32_t>(n) << (4 * h);
+      uint32_t v = 0;
+#pragma unroll
+      for (int j = 0; j < NOUT; ++j) v |= gf_mul_dev(jobs[job0].coef[j][i], x) << (8 * j);
+      lds[((job0 & 1) * kTab + i * kTableBytes + (h ? kHiBase + n * kHiStride : n * 4)) / 4] = v;
+    }
+  }
+  if (threadIdx.x < S) full[threadIdx.x] = 0, freed[threadIdx.x] = 0;
+  if (threadIdx.x < C) prog[threadIdx.x] = threadIdx.x;
+  if (threadIdx.x == 0) {
+    bypass = 0;
+    tab_job = b0 < total ? b0 / RQ : 0;
+    seq_end = b0 < total ? 0xFFFFFFFFu : 0u;
+    nclaimed = b0 < total ? 1u : 0u;
+    claim_end = b0 < total ? 0xFFFFFFFFu : 0u;
+    lbatch = 0;
+  }
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);  // see ring_sweep
+
+  if (wave == 0) {
+    if (b0 < total) {
+      const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lr_u4*) ring)));
+      unsigned pub = 0;
+      auto publish = [&]() {
+        if (lane == 0) ring_flag_st(&full[pub % S], pub / S + 1);
+        ++pub;
+      };
+      auto past = [&](unsigned T) {
+        const bool ok = lane >= C || ring_flag_ld(&prog[lane]) >= T;
+        return __builtin_amdgcn_ballot_w64(!ok) == 0;
+      };
+      unsigned job = b0 / RQ;
+      unsigned last_end[2] = {0u, 0u};  // position after the last job that used each table buffer
+      const uint8_t* in[NIN];
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) in[i] = jobs[job].in[i];
+      unsigned p = 0;
+      bool stop = false;
+      for (unsigned n = 0; !stop; ++n) {
+        // batch n's base from the claimer (claimed ahead; a wait is rare)
+        if (lane == 0) ring_flag_st(&lbatch, n);
+        if (ring_flag_ld(&nclaimed) <= n && ring_flag_ld(&claim_end) > n) {
+          ring_wait_vm<0>();
+          while (pub < p) publish();
+          unsigned spins = 0;
+          while (ring_flag_ld(&nclaimed) <= n && ring_flag_ld(&claim_end) > n && ring_flag_ld(&bypass) == 0u &&
+                 ++spins < kRingSpinCap)
+            __builtin_amdgcn_s_sleep(1);
+          if (spins >= kRingSpinCap || (ring_flag_ld(&nclaimed) <= n && ring_flag_ld(&bypass) != 0u)) {
+            if (lane == 0) {
+              ring_flag_st(&bypass, 1u);
+              if (L.fault) atomicAdd(L.fault, 1u);
+            }
+            stop = true;
+            break;
+          }
+        }
+        if (ring_flag_ld(&nclaimed) <= n) break;  // the queue is empty: the end
+        const unsigned base = __builtin_amdgcn_readfirstlane(ring_flag_ld(&bbase[n % NB]));
+        const unsigned bj = base / RQ;
+        if (bj != job) {
+          // a new job at position p: its tables go to buffer bj & 1, last used
+          // by a job that ended at last_end[bj & 1]
+          last_end[job & 1] = p;
+          job = bj;
+          const unsigned T = last_end[job & 1];
+          if (!past(T)) {
+            ring_wait_vm<0>();
+            while (pub < p) publish();
+            unsigned spins = 0;
+            while (!past(T) && ++spins < kRingHangCap) __builtin_amdgcn_s_sleep(1);
+            if (spins >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+          }
+          build_tables_wave<NIN, NOUT>(lds, (job & 1) * kTab, jobs + job, lane);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          if (lane == 0) ring_flag_st(&tab_job, job);
+#pragma unroll
+          for (int i = 0; i < NIN; ++i) in[i] = jobs[job].in[i];
+        }
+        // rows of this batch: (bq + i) * nq + q (RQ is a multiple of B, so a
+        // batch stays in one job; one division per batch)
+        const unsigned bq = base - bj * RQ;
+        for (unsigned i = 0; i < B; ++i, ++p) {
+          const unsigned use = p / S;
+          if (ring_flag_ld(&freed[p % S]) < use) {
+#if REDSET_RING_DRAIN
+            ring_wait_vm<0>();
+            while (pub < p) publish();
+#endif
+            unsigned spins = 0;
+            while (ring_flag_ld(&freed[p % S]) < use && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+            if (spins >= kRingSpinCap) {
+              // stop: publish what is issued; the consumers take the rest of
+              // the claimed batches directly, then claim on their own
+              ring_wait_vm<0>();
+              while (pub < p) publish();
+              if (lane == 0) {
+                ring_flag_st(&bypass, 1u);
+                if (L.fault) atomicAdd(L.fault, 1u);
+              }
+              stop = true;
+              break;
+            }
+          }
+          const unsigned u = base + i;
+          if (lane == 0) ring_flag_st(&pitem[p % S], u);
+          // (p is uniform; the compiler cannot tell after the capped waits)
+          const uint32_t slot = __builtin_amdgcn_readfirstlane(ring0 + (p % S) * NIN * 1024);
+          const unsigned row = (bq + i) * nq + q;
+          const size_t v = row < rows ? static_cast<size_t>(row) * 64 + lane : 0;
+          const size_t vc = v < nvec ? v : nvec - 1;
+#pragma unroll
+          for (int k = 0; k < NIN; ++k) {
+            uint32_t keep;
+            asm volatile(
+                "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+#if REDSET_LOAD_POLICY == 1
+                " nt"
+#endif
+                "\n\ts_mov_b32 m0, %0"
+                : "=&s"(keep)
+                : "v"((g_cu4*) (in[k]) + vc), "s"(slot + static_cast<uint32_t>(k * 1024))
+                : "memory");
+          }
+          if (p + 1 - pub == static_cast<unsigned>(D)) {
+            ring_wait_vm<(D - 1) * NIN>();
+            publish();
+          }
+        }
+      }
+      ring_wait_vm<0>();
+      while (pub < p) publish();
+      // the positions the consumers may expect: all issued, or (stopped) every
+      // position of the batches claimed so far
+      if (lane == 0) {
+        const unsigned nc = ring_flag_ld(&nclaimed);
+        ring_flag_st(&seq_end, stop && nc * B > p ? nc * B : p);
+      }
+    }
+  } else if (wave == 1) {
+    // claimer: keep up to kLook batches claimed ahead of the loader's batch
+    if (b0 < total) {
+      for (unsigned n = 1;; ++n) {
+        unsigned spins = 0;
+        while (n >= ring_flag_ld(&lbatch) + 1 + kLook && ring_flag_ld(&bypass) == 0u && ++spins < kRingSpinCap)
+          __builtin_amdgcn_s_sleep(2);
+        if (ring_flag_ld(&bypass) != 0u || spins >= kRingSpinCap) {
+          if (spins >= kRingSpinCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+          if (lane == 0) ring_flag_st(&bypass, 1u);
+          break;
+        }
+        unsigned bb = 0;
+        if (lane == 0) bb = atomicAdd(qctr, B);
+        bb = __builtin_amdgcn_readfirstlane(bb);
+        if (bb >= total) {
+          if (lane == 0) ring_flag_st(&claim_end, n);
+          break;
+        }
+        if (lane == 0) {
+          ring_flag_st(&bbase[n % NB], bb);
+          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+          ring_flag_st(&nclaimed, n + 1);
+        }
+      }
+    }
+  } else {
+    // consumers: positions c, c + C, ... of the block's sequence
+    const int c = wave - 2;
+    GfAcc<NOUT, ACC> body;
+    body.lds = lds;
+    g_cu4* in[NIN];
+    int cur = -1;
+    unsigned cur_lo = 0;  // first queue item of job `cur`
+    for (unsigned p = c;; p += C) {
+      const unsigned want = p / S + 1;
+      unsigned spins = 0;
+      bool direct = false, done = false;
+      while (ring_flag_ld(&full[p % S]) < want) {
+        if (p >= ring_flag_ld(&seq_end)) {
+          done = true;
+          break;
+        }
+        if (ring_flag_ld(&bypass) != 0u || ++spins >= kRingSpinCap) {
+          direct = true;
+          break;
+        }
+        __builtin_amdgcn_s_sleep(REDSET_RING_SLEEP);
+      }
+      if (done) break;
+      unsigned u;
+      if (!direct) {
+        u = ring_flag_ld(&pitem[p % S]);
+      } else {
+        if (spins >= kRingSpinCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+        // the position's item from its batch's base once the batch is claimed;
+        // a batch is never claimed once the queue is empty (claim_end) or the
+        // claimer has stopped (BYPASS): then this sequence ends here. Nothing
+        // else keeps the claim back, so the wait ends (hang cap only)
+        unsigned s3 = 0;
+        while (ring_flag_ld(&nclaimed) <= p / B && ring_flag_ld(&claim_end) > p / B && ring_flag_ld(&bypass) == 0u &&
+               ++s3 < kRingHangCap)
+          __builtin_amdgcn_s_sleep(1);
+        if (s3 >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+        if (ring_flag_ld(&nclaimed) <= p / B) break;
+        u = ring_flag_ld(&bbase[(p / B) % NB]) + p % B;
+      }
+      u = __builtin_amdgcn_readfirstlane(u);
+      if (cur < 0 || u - cur_lo >= RQ) {  // another job than the last position's (rare): divide
+        const unsigned jn = u / RQ;
+        cur = static_cast<int>(jn);
+        cur_lo = jn * RQ;
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (jobs[jn].in[i]);
+#pragma unroll
+        for (int j = 0; j < NOUT; ++j) body.out[j] = (g_u4*) (jobs[jn].out[j]);
+      }
+      const unsigned job = static_cast<unsigned>(cur);
+      const unsigned row = (u - cur_lo) * nq + q;
+      const size_t v = static_cast<size_t>(row) * 64 + lane;
+      const bool ok = row < rows && v < nvec;
+      v4u x[NIN];
+      if (!direct) {
+        const lr_u4* sl = (const lr_u4*) ring + (p % S) * NIN * 64;
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) x[i] = sl[i * 64 + lane];
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if (lane == 0) ring_flag_st(&freed[p % S], want);
+      } else {
+        unsigned s2 = 0;
+        while (ring_flag_ld(&freed[p % S]) + 1u < want && ++s2 < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+        if (lane == 0 && ring_flag_ld(&freed[p % S]) + 1u >= want) ring_flag_st(&freed[p % S], want);
+        const size_t vc = ok ? v : nvec - 1;
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) x[i] = ring_direct_load(in[i] + vc);
+      }
+      // this job's tables: wait for them unless the loader has stopped
+      bool tables = true;
+      if (ring_flag_ld(&tab_job) < job) {
+        unsigned s4 = 0;
+        while (ring_flag_ld(&tab_job) < job && ring_flag_ld(&bypass) == 0u && ++s4 < kRingSpinCap)
+          __builtin_amdgcn_s_sleep(REDSET_RING_SLEEP);
+        tables = ring_flag_ld(&tab_job) >= job;
+      }
+      if (ok) {
+        if (tables) {
+          body.begin();
+          if (job & 1) body.template add<0, NIN, kTab>(x);
+          else body.template add<0, NIN, 0>(x);
+          body.finish(v);
+        } else {
+          gf_mac_vec_slow<NIN, NOUT, ACC>(jobs + job, in, v);
+        }
+      }
+      if (lane == 0) ring_flag_st(&prog[c], p + C);
+    }
+    if (lane == 0) ring_flag_st(&prog[c], 0xFFFFFFFFu);
+    // the loader stopped early: claim what is left, batch by batch, and
+    // compute it without tables
+    if (ring_flag_ld(&bypass) != 0u) {
+      while (true) {
+        unsigned bb = 0;
+        if (lane == 0) bb = atomicAdd(qctr, B);
+        bb = __builtin_amdgcn_readfirstlane(bb);
+        if (bb >= total) break;
+        const unsigned job = bb / RQ;
+        g_cu4* jin[NIN];
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) jin[i] = (g_cu4*) (jobs[job].in[i]);
+        for (unsigned i = 0; i < B; ++i) {
+          const unsigned u = bb + i;
+          const size_t v = vec_of(u);
+          if (row_ok(u) && v < nvec) gf_mac_vec_slow<NIN, NOUT, ACC>(jobs + job, jin, v);
+        }
+      }
+    }
+  }
+  // every claim of this block is done: count it; the launch's last block
+  // zeroes the queues for the next launch (stream order makes it visible)
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    __threadfence();
+    const unsigned done = atomicAdd(fin, 1u);
+    if (done == gridDim.x - 1) {
+      __threadfence();
+      for (int k = 0; k < kClaimQueues; ++k) atomicExch(L.claim + k * kClaimStride, 0u);
+      atomicExch(fin, 0u);
+    }
+  }
+}
+#endif
 
 template <int NIN, bool ACC>
 __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, int part) {
@@ -1098,12 +1763,24 @@ struct BlockClock {
 template <int NIN, int NOUT, bool ACC>
 REDSET_KERNEL gf_mac_kernel(GfLaunch L) {
   BlockClock clock(L.fault);
-  if (L.sequential == kJobsInKernel) {
+#if REDSET_RING
+  if constexpr (NIN <= 8 && REDSET_RING_GF_ROWS == 1) {
+    if (L.sequential == kJobsStreamed && !L.bytes_only && L.nbytes % 16 == 0) {
+      gf_mac_stream<NIN, NOUT, ACC>(L);
+      return;
+    }
+    if (L.sequential == kJobsClaimed && L.claim && !L.bytes_only && L.nbytes % 16 == 0) {
+      gf_mac_claimed<NIN, NOUT, ACC>(L);
+      return;
+    }
+  }
+#endif
+  if (L.sequential == kJobsInKernel || L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) {
     // every block sweeps every job in turn: one stripe's cells in flight at
     // a time, with no launch boundary between stripes
     for (int j = 0; j < L.njobs; ++j) {
       if (j > 0) __syncthreads();  // all waves are done with the last job's tables
-      gf_mac_body<NIN, NOUT, ACC>(L, L.jobs[j], blockIdx.x);
+      gf_mac_body<NIN, NOUT, ACC>(L, L.jobs[L.job0 + j], blockIdx.x);
     }
     return;
   }
@@ -1119,8 +1796,8 @@ REDSET_KERNEL gf_mac_kernel_arg(GfLaunch L, GfJob J) {
 template <int NIN, bool ACC>
 REDSET_KERNEL xor_kernel(XorLaunch L) {
   BlockClock clock(L.fault);
-  if (L.sequential == kJobsInKernel) {
-    for (int j = 0; j < L.njobs; ++j) xor_body<NIN, ACC>(L, L.jobs[j], blockIdx.x);
+  if (L.sequential == kJobsInKernel || L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) {
+    for (int j = 0; j < L.njobs; ++j) xor_body<NIN, ACC>(L, L.jobs[L.job0 + j], blockIdx.x);
     return;
   }
   const int job = blockIdx.x / L.blocks_per_job;

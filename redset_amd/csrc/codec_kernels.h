@@ -21,6 +21,20 @@ constexpr int kMaxOut = 4;
 // last two keep one stripe's cells in flight at a time.
 constexpr int kJobsInLaunches = 1;
 constexpr int kJobsInKernel = 2;
+// kJobsStreamed: one launch whose blocks stream their items of all the jobs
+// through one continuous loader ring (codec_device.h gf_mac_stream; GF jobs
+// of <= 8 inputs over whole 16-B vectors, else as kJobsInKernel).
+constexpr int kJobsStreamed = 3;
+// kJobsClaimed: as kJobsStreamed, but the blocks of each XCD claim their
+// items in batches from a shared per-XCD queue (GfLaunch::claim), so no block
+// runs ahead of the others or idles at the end (codec_device.h gf_mac_claimed).
+constexpr int kJobsClaimed = 4;
+// claim queues: one counter per XCD, 128 B apart, then the finished-block
+// counter (kClaimWords words per launch, zeroed by the planner; the last
+// block of a launch zeroes them again)
+constexpr int kClaimQueues = 8;
+constexpr int kClaimStride = 32;
+constexpr int kClaimWords = (kClaimQueues + 1) * kClaimStride;
 
 // One stripe (or one pass over a slice of a stripe's members):
 // out[j] (^)= sum_i coef[j][i] * in[i] over GF(2^8), byte by byte.
@@ -41,9 +55,11 @@ struct GfLaunch {
   int blocks_per_job;
   int sequential;           // job order: 0 side by side, kJobsInLaunches, kJobsInKernel (launch_gf)
   int job0;                 // first job of this launch (set by the launcher)
-  int group;                // kJobsInLaunches: jobs per launch, side by side (0 = 1)
+  int group;                // kJobsInLaunches: jobs per launch, side by side (0 = 1);
+                            // kJobsStreamed / kJobsClaimed: jobs per launch, in turn (0 = all)
   size_t nbytes;            // bytes per cell
   unsigned* fault;          // set by the launcher: counts capped ring spins (codec_device.h)
+  unsigned* claim;          // kJobsClaimed: kClaimWords zeroed device words (planner)
 };
 
 // XOR of `nin` inputs into one output (the XOR scheme's parity / rebuild).

@@ -34,6 +34,7 @@ const KernelSet& kernel_set(int nin) {
 // jobs one launch covers (the last launch may get fewer)
 template <class Launch>
 int jobs_per_launch(const Launch& L) {
+  if (L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) return L.group > 0 ? L.group : L.njobs;
   return L.sequential == kJobsInLaunches ? std::max(1, L.group) : L.njobs;
 }
 
@@ -128,7 +129,10 @@ int launch_gf(const GfLaunch& L, void* stream) {
     GfLaunch one = L;
     one.job0 = j;
     one.fault = ring_fault_word();
-    const int n = L.sequential == kJobsInKernel ? 1 : std::min(per, L.njobs - j);
+    if (L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) one.njobs = std::min(per, L.njobs - j);
+    const int n = (L.sequential == kJobsInKernel || L.sequential == kJobsStreamed || L.sequential == kJobsClaimed)
+                      ? 1
+                      : std::min(per, L.njobs - j);
     const dim3 grid(static_cast<unsigned>(n * L.blocks_per_job));
     hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), one);
     const hipError_t e = hipGetLastError();
@@ -166,7 +170,10 @@ int launch_xor(const XorLaunch& L, void* stream) {
     XorLaunch one = L;
     one.job0 = j;
     one.fault = ring_fault_word();
-    const int n = L.sequential == kJobsInKernel ? 1 : std::min(per, L.njobs - j);
+    if (L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) one.njobs = std::min(per, L.njobs - j);
+    const int n = (L.sequential == kJobsInKernel || L.sequential == kJobsStreamed || L.sequential == kJobsClaimed)
+                      ? 1
+                      : std::min(per, L.njobs - j);
     const dim3 grid(static_cast<unsigned>(n * L.blocks_per_job));
     hipLaunchKernelGGL(k, grid, dim3(kBlock), 0, static_cast<hipStream_t>(stream), one);
     const hipError_t e = hipGetLastError();

@@ -40,6 +40,7 @@ struct redset_hip_plan {
   redset_hip_plan_info info{};
   GfJob* d_gf = nullptr;  // device job arrays
   XorJob* d_xor = nullptr;
+  unsigned* d_claim = nullptr;  // kJobsClaimed launches' queue counters
   std::vector<GfLaunch> gf_launches;
   std::vector<XorLaunch> xor_launches;
 };
@@ -94,31 +95,57 @@ int xor_blocks_cap() {
 // (5.43 vs 5.16) and 32 MiB (5.46 vs 5.11); grouping 2-6 stripes per launch
 // never beats both (profiles/r01_sequential_jobs.txt, cell-size sweeps). Sets
 // with smaller cells keep their stripes side by side in one launch (0).
-// REDSET_HIP_SEQUENTIAL=0 / 1 / 2 forces an order (A/B, tests); read at every
-// plan build.
+// Round 3, with the loader ring: GF stripes of <= 8 inputs over whole 16-B
+// vectors (RS(8+3) encode and rebuild) go two per launch, streamed through
+// one continuous ring (kJobsStreamed, codec_device.h gf_mac_stream): a block
+// that finishes its share of the first stripe goes straight on to the
+// second, so a pair pays one launch gap and one tail instead of two; +1.5 to
+// +2.5% on the RS(8+3) step against one launch per stripe. Streaming more
+// stripes per launch loses (4: +1%; all 11: -3.5%: blocks drift apart and
+// sweep different stripes at once); claiming the items at run time instead
+// (kJobsClaimed) keeps the blocks together, but costs the rebuild 3% more
+// than it gains the encode (profiles/r03_ab_stream.txt).
+// REDSET_HIP_SEQUENTIAL=0..4 forces an order (A/B, tests; XOR launches take
+// 1 for 3 and 4); REDSET_HIP_STREAM_JOBS sets the stripes per streamed or
+// claimed launch (0 = all). Read at every plan build.
 constexpr size_t kSequentialMinCell = 24u << 20;
 
-int sequential_jobs(int njobs, size_t nbytes) {
+int sequential_jobs(int njobs, size_t nbytes, bool gf, bool streamable) {
   if (njobs < 2) return 0;
+  int order = nbytes >= kSequentialMinCell ? (gf && streamable ? redset_hip::kJobsStreamed : redset_hip::kJobsInLaunches)
+                                           : 0;
   const char* s = std::getenv("REDSET_HIP_SEQUENTIAL");
-  if (s && s[0] >= '0' && s[0] <= '2' && s[1] == '\0') return s[0] - '0';
-  return nbytes >= kSequentialMinCell ? redset_hip::kJobsInLaunches : 0;
+  if (s && s[0] >= '0' && s[0] <= '4' && s[1] == '\0') order = s[0] - '0';
+  if ((order == redset_hip::kJobsStreamed || order == redset_hip::kJobsClaimed) && !(gf && streamable))
+    order = redset_hip::kJobsInLaunches;
+  return order;
 }
 
-// Stripes per launch in sequence mode (side by side within the launch);
-// REDSET_HIP_STRIPES_PER_LAUNCH overrides the default of 1 (A/B).
-int stripes_per_launch() {
+// Stripes per launch: in sequence mode side by side within the launch
+// (REDSET_HIP_STRIPES_PER_LAUNCH, default 1); streamed or claimed, one after
+// another through the ring (REDSET_HIP_STREAM_JOBS, default 2, 0 = all).
+int stripes_per_launch(int order) {
+  if (order == redset_hip::kJobsStreamed || order == redset_hip::kJobsClaimed) {
+    const char* s = std::getenv("REDSET_HIP_STREAM_JOBS");
+    return (s && s[0] >= '0' && s[0] <= '9') ? std::atoi(s) : 2;
+  }
   const char* s = std::getenv("REDSET_HIP_STRIPES_PER_LAUNCH");
   return (s && std::atoi(s) > 0) ? std::atoi(s) : 1;
 }
 
 int launches_of(int order, int njobs, int group) {
+  if (order == redset_hip::kJobsStreamed || order == redset_hip::kJobsClaimed)
+    return group > 0 ? (njobs + group - 1) / group : 1;
   return order == redset_hip::kJobsInLaunches ? (njobs + group - 1) / group : 1;
 }
 
 // jobs that share one launch's grid
 int jobs_sharing_grid(int order, int njobs, int group) {
-  return order == redset_hip::kJobsInLaunches ? std::min(group, njobs) : order == redset_hip::kJobsInKernel ? 1 : njobs;
+  return order == redset_hip::kJobsInLaunches                                            ? std::min(group, njobs)
+         : (order == redset_hip::kJobsInKernel || order == redset_hip::kJobsStreamed ||
+            order == redset_hip::kJobsClaimed)
+             ? 1
+                                                                                       : njobs;
 }
 
 // Blocks per job so the whole launch fits in one resident wave of blocks.
@@ -223,8 +250,8 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     G.accumulate = P.accumulate;
     G.bytes_only = P.bytes_only;
     G.nbytes = nbytes;
-    G.sequential = sequential_jobs(G.njobs, nbytes);
-    G.group = stripes_per_launch();
+    G.sequential = sequential_jobs(G.njobs, nbytes, true, P.nin <= 8 && !P.bytes_only && nbytes % 16 == 0);
+    G.group = stripes_per_launch(G.sequential);
     G.blocks_per_job = blocks_per_job(jobs_sharing_grid(G.sequential, G.njobs, G.group), nbytes,
                                       redset_hip::gf_blocks_per_cu(P.nin));
     gall.insert(gall.end(), P.jobs.begin(), P.jobs.end());
@@ -240,8 +267,8 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     X.accumulate = P.accumulate;
     X.bytes_only = P.bytes_only;
     X.nbytes = nbytes;
-    X.sequential = sequential_jobs(X.njobs, nbytes);
-    X.group = stripes_per_launch();
+    X.sequential = sequential_jobs(X.njobs, nbytes, false, false);
+    X.group = stripes_per_launch(X.sequential);
     X.blocks_per_job = blocks_per_job(jobs_sharing_grid(X.sequential, X.njobs, X.group), nbytes, xor_blocks_cap());
     xall.insert(xall.end(), P.jobs.begin(), P.jobs.end());
     plan->xor_launches.push_back(X);
@@ -256,6 +283,19 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
                            "hipMemcpy(plan jobs)"))
       return rc;
     for (GfLaunch& G : plan->gf_launches) G.jobs = plan->d_gf + reinterpret_cast<uintptr_t>(G.jobs);
+  }
+  // claimed launches (the kernel takes them over whole 16-B vectors and <= 8
+  // inputs only, as the streamed ones): their queue counters, zeroed
+  size_t nclaim = 0;
+  for (GfLaunch& G : plan->gf_launches)
+    if (G.sequential == redset_hip::kJobsClaimed) ++nclaim;
+  if (nclaim > 0) {
+    const size_t bytes = nclaim * redset_hip::kClaimWords * sizeof(unsigned);
+    if (int rc = hip_check(hipMalloc(&plan->d_claim, bytes), "hipMalloc(claim queues)")) return rc;
+    if (int rc = hip_check(hipMemset(plan->d_claim, 0, bytes), "hipMemset(claim queues)")) return rc;
+    size_t k = 0;
+    for (GfLaunch& G : plan->gf_launches)
+      if (G.sequential == redset_hip::kJobsClaimed) G.claim = plan->d_claim + (k++) * redset_hip::kClaimWords;
   }
   if (!xall.empty()) {
     if (int rc = hip_check(hipMalloc(&plan->d_xor, xall.size() * sizeof(XorJob)), "hipMalloc(plan jobs)")) return rc;
@@ -497,6 +537,7 @@ void redset_hip_plan_destroy(redset_hip_plan* plan) {
   if (!plan) return;
   if (plan->d_gf) (void) hipFree(plan->d_gf);
   if (plan->d_xor) (void) hipFree(plan->d_xor);
+  if (plan->d_claim) (void) hipFree(plan->d_claim);
   delete plan;
 }
 

@@ -255,14 +255,19 @@ def test_xor_encode_and_rebuild(rd, oracle, p, chunk, padded):
 
 
 @pytest.mark.parametrize("mode,group,n_rs,n_xor", [("0", "1", 1, 1), ("1", "1", 11, 8), ("1", "3", 4, 3),
-                                                   ("2", "1", 1, 1)])
+                                                   ("2", "1", 1, 1), ("3", "2", 6, 4), ("3", "0", 1, 8),
+                                                   ("3", "1", 11, 8), ("4", "0", 1, 8), ("4", "3", 4, 3)])
 def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     """A plan runs its stripes side by side in one launch (REDSET_HIP_SEQUENTIAL=0),
-    one launch per stripe (=1, the default for cells >= 16 MiB; or per
-    REDSET_HIP_STRIPES_PER_LAUNCH stripes) or one launch whose blocks sweep the
-    stripes in turn (=2): same bytes."""
+    one launch per stripe (=1, the default for cells >= 24 MiB but RS(8+3)'s; or
+    per REDSET_HIP_STRIPES_PER_LAUNCH stripes), one launch whose blocks sweep the
+    stripes in turn (=2), `group` stripes per launch streamed through one
+    continuous ring (=3, RS(8+3)'s default: 2; REDSET_HIP_STREAM_JOBS, 0 = all)
+    or the same with the items claimed at run time (=4); XOR plans take =1 for
+    3 and 4: same bytes."""
     monkeypatch.setenv("REDSET_HIP_SEQUENTIAL", mode)
     monkeypatch.setenv("REDSET_HIP_STRIPES_PER_LAUNCH", group)
+    monkeypatch.setenv("REDSET_HIP_STREAM_JOBS", group)
     p, e, chunk, lost = 11, 3, 40_000, [0, 5, 9]
     lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=41)
     lay = upload_set(rd, lofi, parity, p - e, e, chunk)
@@ -295,7 +300,7 @@ def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     assert all(np.array_equal(a, b) for a, b in zip(xgot, xc))
 
 
-@pytest.mark.parametrize("mode", ["2", "0", "1"])
+@pytest.mark.parametrize("mode", ["2", "0", "1", "3", "4"])
 def test_ring_jobs_back_to_back(rd, oracle, monkeypatch, mode):
     """The kernels' loader-wave ring is reused job after job inside one launch
     (REDSET_HIP_SEQUENTIAL=2: every block loops over the stripes) and launch

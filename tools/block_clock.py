@@ -85,10 +85,28 @@ def run(name, plan, reps, launches):
     for _ in range(reps):
         plan.execute()
         out.append(summarize(read_clock()))
+    # is a slow block slow again next launch? end times per CU (XCC_ID, HW_ID's
+    # SE / SH / CU fields) across launches
+    ends = []
+    for _ in range(reps):
+        plan.execute()
+        rows = read_clock()
+        t0 = rows[:, 0].astype(np.int64)
+        hw = rows[:, 2].astype(np.int64)
+        cu_key = ((hw >> 32) << 16) | ((hw & 0xFFFF) >> 8)  # xcc | se/sh/cu bits of HW_ID
+        e = {int(k): float(v) for k, v in zip(cu_key, (rows[:, 1].astype(np.int64) - t0.min()) * TICK_US)}
+        ends.append(e)
+    common = sorted(set.intersection(*[set(e) for e in ends]))
+    M = np.array([[e[k] for k in common] for e in ends])
+    M = M - M.mean(axis=1, keepdims=True)
+    corr = [float(np.corrcoef(M[i], M[i + 1])[0, 1]) for i in range(len(M) - 1)]
+    persist = {"cus": len(common), "end_corr_consecutive_mean": round(float(np.mean(corr)), 3),
+               "per_cu_mean_end_spread_us": round(float(M.mean(axis=0).max() - M.mean(axis=0).min()), 2),
+               "per_launch_end_spread_us": round(float(np.mean(M.max(axis=1) - M.min(axis=1))), 2)}
     keys = ("ramp_us", "span_us", "busy_mean_us", "edge_idle_frac")
     mean = {k: round(float(np.mean([o[k] for o in out])), 4) for k in keys}
     print(json.dumps({"case": name, "lib": _lib.LIB_PATH, "event_us_per_launch": ev, "mean": mean,
-                      "last": out[-1]}), flush=True)
+                      "persistence": persist, "last": out[-1]}), flush=True)
 
 
 def main():

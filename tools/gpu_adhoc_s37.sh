@@ -1,0 +1,16 @@
+# streamed launches: all stripes in one launch vs 1 / 2 / 4 stripes per launch, against launch-per-stripe
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+OUT=gpurun_out/r03s37; mkdir -p $OUT; rm -f $OUT/ab.jsonl
+for r in 1 2; do
+  for m in "1 0" "3 0" "3 1" "3 2" "3 4"; do
+    set -- $m
+    REDSET_HIP_SEQUENTIAL=$1 REDSET_HIP_STREAM_JOBS=$2 timeout -k 10 150 python bench.py --steps 20 --warmup 5 --cpu-baseline 0 --pairs 0 > $OUT/b.tmp 2> $OUT/b.err || exit 1
+    echo "seq$1/sj$2 $(tail -1 $OUT/b.tmp)" >> $OUT/ab.jsonl
+  done
+done
+python3 - <<'PY'
+import json
+for line in open("gpurun_out/r03s37/ab.jsonl"):
+    t, js = line.split(" ", 1); r = json.loads(js); b = r["breakdown"]
+    print(f"{t:9s} step {r['value']:7.1f} encode {b['encode_GBps']:7.1f} rebuild {b['rebuild_GBps']:7.1f} xor {r['xor']['value']:7.1f} rt {r['round_trip_bit_exact']} faults {r['ring_faults']}")
+PY

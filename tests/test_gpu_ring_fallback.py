@@ -48,16 +48,24 @@ def test_gpu_suite_bit_exact_with_ring_fallbacks(tmp_path):
         "REDSET_RING_FALLBACK_RUN": "1",
         "REDSET_RING_FAULT_LOG": str(log),
     })
-    res = subprocess.run(
-        [sys.executable, "-u", "-m", "pytest", os.path.join(ROOT, "tests"), "-m", "gpu", "-x", "-q",
-         "-p", "no:cacheprovider", "--timeout", "300", "--timeout-method", "thread",
-         "--deselect", "tests/test_gpu_ring_fallback.py::test_gpu_suite_bit_exact_with_ring_fallbacks"],
-        cwd=ROOT, env=env, capture_output=True, text=True, timeout=1150)
-    tail = (res.stdout + res.stderr)[-6000:]
-    assert res.returncode == 0, tail
+    # the child's report goes to a file as it runs (REDSET_TEST_PROGRESS_DIR, if
+    # set, else the test's tmp dir), one line per test, so a long run shows
+    # progress to whoever watches that directory
+    out_dir = os.environ.get("REDSET_TEST_PROGRESS_DIR") or str(tmp_path)
+    os.makedirs(out_dir, exist_ok=True)
+    child_log = os.path.join(out_dir, "spincap_twin_suite.log")
+    with open(child_log, "w") as f:
+        res = subprocess.run(
+            [sys.executable, "-u", "-m", "pytest", os.path.join(ROOT, "tests"), "-m", "gpu", "-x", "-v",
+             "-p", "no:cacheprovider", "--timeout", "300", "--timeout-method", "thread",
+             "--deselect", "tests/test_gpu_ring_fallback.py::test_gpu_suite_bit_exact_with_ring_fallbacks"],
+            cwd=ROOT, env=env, stdout=f, stderr=subprocess.STDOUT, text=True, timeout=1150)
+    with open(child_log) as f:
+        text = f.read()
+    assert res.returncode == 0, text[-6000:]
     lines = log.read_text().split()
     faults, libs = int(lines[0]), lines[1:]
-    print(f"spin-cap twin: {faults} capped spins; mapped {libs}; {res.stdout.strip().splitlines()[-1]}")
+    print(f"spin-cap twin: {faults} capped spins; mapped {libs}; {text.strip().splitlines()[-1]}")
     assert libs == [TWIN], libs
     # thousands of launches, each with a capped handshake or several
     assert faults > 1000, faults

@@ -11,7 +11,7 @@ mkdir -p "$OUT"
 ok() { local s=$1; [ "$s" -eq 0 ] || [ "$s" -eq 1 ]; }
 
 echo "== gpu tests" | tee "$OUT/progress.txt"
-timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread "$@" > "$OUT/gpu_tests.log" 2>&1
+REDSET_TEST_PROGRESS_DIR="$OUT" timeout -k 10 900 python -u -m pytest tests -m gpu -q -x --timeout 120 --timeout-method thread "$@" > "$OUT/gpu_tests.log" 2>&1
 s=$?; echo "gpu tests exit $s" | tee -a "$OUT/progress.txt"; tail -3 "$OUT/gpu_tests.log"
 ok $s || exit $s
 

@@ -1668,6 +1668,174 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
 }
 #endif
 
+#if REDSET_RING
+// kJobsStreamed for XOR (see gf_mac_stream): the launch's jobs through one
+// continuous ring, item g of a block = item g % K of job g / K; no tables, so
+// no hand-over between jobs. Same items (R rows), depth and fallbacks as
+// xor_body's ring_sweep.
+// the XOR kernels' ring, one static array shared by xor_body and xor_stream
+template <int NIN, int R>
+__device__ __forceinline__ v4u* xor_lds() {
+  __shared__ v4u ring[ring_vecs<NIN, R>()];
+  return ring;
+}
+
+template <int NIN, bool ACC>
+__device__ __forceinline__ void xor_stream(const XorLaunch& L) {
+  constexpr int R = NIN > REDSET_RING_XOR_WIDE ? 1 : REDSET_RING_XOR_ROWS;
+  constexpr int D =
+      ring_depth<NIN, R, R == 1 ? REDSET_RING_XOR_ROWS_IN_FLIGHT : REDSET_RING_ROWS_IN_FLIGHT>();
+  constexpr int S = ring_slots<NIN * R>();
+  constexpr int C = kBlock / 64 - 1;
+  static_assert(D >= 2 && D - 1 < S && (D - 1) * NIN * R <= 63, "ring depth");
+  typedef __attribute__((address_space(4))) const XorJob c_job;
+  const c_job* const jobs = (const c_job*) (L.jobs + L.job0);
+  v4u* const ring = xor_lds<NIN, R>();
+  __shared__ unsigned full[S], freed[S], bypass;
+
+  const size_t nvec = L.nbytes / 16;
+  const size_t G = gridDim.x;
+  const size_t part = blockIdx.x;
+  const size_t rows = (nvec + 63) / 64;
+  const size_t items = (rows + R - 1) / R;
+  const unsigned K = items > part ? static_cast<unsigned>((items - part + G - 1) / G) : 0u;
+  const unsigned total = K * static_cast<unsigned>(L.njobs);
+  if (K == 0) return;
+  if (threadIdx.x < S) full[threadIdx.x] = 0, freed[threadIdx.x] = 0;
+  if (threadIdx.x == 0) bypass = 0;
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);  // see ring_sweep
+  const int wave = __builtin_amdgcn_readfirstlane(static_cast<int>(threadIdx.x) >> 6);
+  const int lane = threadIdx.x & 63;
+  auto vec_of = [&](unsigned k, int r) { return ((static_cast<size_t>(k) * G + part) * R + r) * 64 + lane; };
+
+  if (wave == 0) {
+    const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lr_u4*) ring)));
+    unsigned pub = 0;
+    auto publish = [&]() {
+      if (lane == 0) ring_flag_st(&full[pub % S], pub / S + 1);
+      ++pub;
+    };
+    const uint8_t* in[NIN];
+#pragma unroll
+    for (int i = 0; i < NIN; ++i) in[i] = jobs[0].in[i];
+    unsigned job = 0, k = 0;
+    for (unsigned g = 0; g < total; ++g, ++k) {
+      if (k == K) {
+        k = 0;
+        ++job;
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) in[i] = jobs[job].in[i];
+      }
+      const unsigned use = g / S;
+      if (ring_flag_ld(&freed[g % S]) < use) {
+#if REDSET_RING_DRAIN
+        ring_wait_vm<0>();
+        while (pub < g) publish();
+#endif
+        unsigned spins = 0;
+        while (ring_flag_ld(&freed[g % S]) < use && ++spins < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+        if (spins >= kRingSpinCap) {
+          ring_wait_vm<0>();
+          while (pub < g) publish();
+          if (lane == 0) {
+            ring_flag_st(&bypass, 1u);
+            if (L.fault) atomicAdd(L.fault, 1u);
+          }
+          return;
+        }
+      }
+      const uint32_t slot = ring0 + (g % S) * NIN * R * 1024;
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const size_t v = vec_of(k, r);
+        const size_t vc = v < nvec ? v : nvec - 1;
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) {
+          uint32_t keep;
+          asm volatile(
+              "s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off"
+#if REDSET_LOAD_POLICY == 1
+              " nt"
+#endif
+              "\n\ts_mov_b32 m0, %0"
+              : "=&s"(keep)
+              : "v"((g_cu4*) (in[i]) + vc), "s"(slot + static_cast<uint32_t>((i * R + r) * 1024))
+              : "memory");
+        }
+      }
+      if (g + 1 - pub == static_cast<unsigned>(D)) {
+        ring_wait_vm<(D - 1) * NIN * R>();
+        publish();
+      }
+    }
+    ring_wait_vm<0>();
+    while (pub < total) publish();
+    return;
+  }
+
+  const int c = wave - 1;
+  XorAcc<ACC> body;
+  g_cu4* in[NIN];
+  int cur = -1;
+  unsigned job = static_cast<unsigned>(c) / K, k = static_cast<unsigned>(c) % K;
+  for (unsigned g = c; g < total; g += C) {
+    if (static_cast<int>(job) != cur) {
+      cur = static_cast<int>(job);
+#pragma unroll
+      for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (jobs[job].in[i]);
+      body.out = (g_u4*) (jobs[job].out);
+    }
+    const unsigned want = g / S + 1;
+    unsigned spins = 0;
+    bool direct = false;
+    while (ring_flag_ld(&full[g % S]) < want) {
+      if (ring_flag_ld(&bypass) != 0u || ++spins >= kRingSpinCap) {
+        direct = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(REDSET_RING_SLEEP);
+    }
+    if (direct) {
+      // as in ring_sweep
+      if (spins >= kRingSpinCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+      unsigned s2 = 0;
+      while (ring_flag_ld(&freed[g % S]) + 1u < want && ++s2 < kRingSpinCap) __builtin_amdgcn_s_sleep(1);
+      if (lane == 0 && ring_flag_ld(&freed[g % S]) + 1u >= want) ring_flag_st(&freed[g % S], want);
+    }
+    const lr_u4* sl = (const lr_u4*) ring + (g % S) * NIN * R * 64;
+    v4u x[R][NIN];
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if (!direct) {
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) x[r][i] = sl[(i * R + r) * 64 + lane];
+      } else {
+        const size_t v = vec_of(k, r);
+        const size_t vc = v < nvec ? v : nvec - 1;
+#pragma unroll
+        for (int i = 0; i < NIN; ++i) x[r][i] = ring_direct_load(in[i] + vc);
+      }
+    }
+    if (!direct) {
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      if (lane == 0) ring_flag_st(&freed[g % S], want);
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const size_t v = vec_of(k, r);
+      if (v < nvec) {
+        body.begin();
+        body.template add<0>(x[r]);
+        body.finish(v);
+      }
+    }
+    k += C;
+    while (k >= K) k -= K, ++job;
+  }
+}
+#endif
+
 template <int NIN, bool ACC>
 __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, int part) {
   const size_t nvec = L.bytes_only ? 0 : L.nbytes / 16;
@@ -1683,7 +1851,7 @@ __device__ __forceinline__ void xor_body(const XorLaunch& L, const XorJob& J, in
     // the GF kernels' one-row shape
     constexpr int kRows = NIN > REDSET_RING_XOR_WIDE ? 1 : REDSET_RING_XOR_ROWS;
     constexpr int kDepth = ring_depth<NIN, kRows, kRows == 1 ? REDSET_RING_XOR_ROWS_IN_FLIGHT : REDSET_RING_ROWS_IN_FLIGHT>();
-    __shared__ v4u ring[ring_vecs<NIN, kRows>()];
+    v4u* const ring = xor_lds<NIN, kRows>();
     XorAcc<ACC> body;
     body.out = out;
     ring_sweep<NIN, kRows, kDepth>(ring, in, nvec, static_cast<size_t>(L.blocks_per_job),
@@ -1796,6 +1964,14 @@ REDSET_KERNEL gf_mac_kernel_arg(GfLaunch L, GfJob J) {
 template <int NIN, bool ACC>
 REDSET_KERNEL xor_kernel(XorLaunch L) {
   BlockClock clock(L.fault);
+#if REDSET_RING
+  if constexpr (NIN <= REDSET_RING_CHUNK) {
+    if (L.sequential == kJobsStreamed && !L.bytes_only && L.nbytes % 16 == 0) {
+      xor_stream<NIN, ACC>(L);
+      return;
+    }
+  }
+#endif
   if (L.sequential == kJobsInKernel || L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) {
     for (int j = 0; j < L.njobs; ++j) xor_body<NIN, ACC>(L, L.jobs[L.job0 + j], blockIdx.x);
     return;

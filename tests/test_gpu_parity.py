@@ -255,7 +255,7 @@ def test_xor_encode_and_rebuild(rd, oracle, p, chunk, padded):
 
 
 @pytest.mark.parametrize("mode,group,n_rs,n_xor", [("0", "1", 1, 1), ("1", "1", 11, 8), ("1", "3", 4, 3),
-                                                   ("2", "1", 1, 1), ("3", "2", 6, 4), ("3", "0", 1, 8),
+                                                   ("2", "1", 1, 1), ("3", "2", 6, 4), ("3", "0", 1, 1),
                                                    ("3", "1", 11, 8), ("4", "0", 1, 8), ("4", "3", 4, 3)])
 def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     """A plan runs its stripes side by side in one launch (REDSET_HIP_SEQUENTIAL=0),
@@ -263,8 +263,8 @@ def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     per REDSET_HIP_STRIPES_PER_LAUNCH stripes), one launch whose blocks sweep the
     stripes in turn (=2), `group` stripes per launch streamed through one
     continuous ring (=3, RS(8+3)'s default: 2; REDSET_HIP_STREAM_JOBS, 0 = all)
-    or the same with the items claimed at run time (=4); XOR plans take =1 for
-    3 and 4: same bytes."""
+    or the same with the items claimed at run time (=4; XOR plans take =1
+    there): same bytes."""
     monkeypatch.setenv("REDSET_HIP_SEQUENTIAL", mode)
     monkeypatch.setenv("REDSET_HIP_STRIPES_PER_LAUNCH", group)
     monkeypatch.setenv("REDSET_HIP_STREAM_JOBS", group)

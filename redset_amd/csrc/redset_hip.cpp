@@ -137,11 +137,13 @@ int stripes_per_launch(int order) {
   return (s && std::atoi(s) > 0) ? std::atoi(s) : 1;
 }
 
-// XOR plans stream their stripes in pairs by default too (A/B knob
-// REDSET_HIP_XOR_STREAM=0 keeps a launch per stripe)
+// XOR plans keep a launch per stripe: streamed pairs (xor_stream) measured
+// within the XOR leg's run-to-run spread, 6.26 against 6.30 TB/s over three
+// alternating pairs (profiles/r03_ab_stream.txt). A/B knob:
+// REDSET_HIP_XOR_STREAM=1 streams them in pairs.
 bool xor_stream_default() {
   const char* s = std::getenv("REDSET_HIP_XOR_STREAM");
-  return !(s && s[0] == '0');
+  return s && s[0] == '1';
 }
 
 int launches_of(int order, int njobs, int group) {

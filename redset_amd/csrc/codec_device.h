@@ -1319,11 +1319,10 @@ __device__ __forceinline__ void gf_mac_vec_slow(const __attribute__((address_spa
 // Wave 1 is the claimer: it keeps up to kLook batches claimed ahead of the
 // loader (bbase[], nclaimed; its atomic's wait stalls only itself -- in the
 // loader a returning atomic would drain the LDS-DMA queue with vmcnt(0)).
-// Ring position p holds item bbase[(p / B) % NB] + p % B (the loader also
-// records it in pitem[] before publishing). Waves 2-15 consume.
-// Fallbacks (capped waits): a consumer loads an unpublished position straight
-// from HBM, its item from bbase[] (not overwritten before every position of
-// that batch was released: NB * B >= S + (kLook + 1) * B); a capped loader
+// Ring position p holds item bbase[(p / B) % NB] + p % B. Waves 2-15 consume.
+// bbase[] entries are not overwritten before every position of their batch
+// was released (NB * B >= S + (kLook + 1) * B). Fallbacks (capped waits): a
+// consumer loads an unpublished position straight from HBM; a capped loader
 // stops (BYPASS), the claimer stops, the consumers finish the claimed
 // batches and then claim batches themselves, computing without tables where
 // the loader never built them (gf_mac_vec_slow). Capped waits are counted.
@@ -1345,7 +1344,7 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
   v4u* const smem = gf_lds<NIN>();
   uint32_t* const lds = reinterpret_cast<uint32_t*>(smem);
   v4u* const ring = smem + kTableVecs;
-  __shared__ unsigned full[S], freed[S], pitem[S], prog[C], bbase[NB];
+  __shared__ unsigned full[S], freed[S], prog[C], bbase[NB];
   __shared__ unsigned bypass, tab_job, seq_end, nclaimed, claim_end, lbatch, first;
 
   const size_t nvec = L.nbytes / 16;
@@ -1481,8 +1480,6 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
               break;
             }
           }
-          const unsigned u = base + i;
-          if (lane == 0) ring_flag_st(&pitem[p % S], u);
           // (p is uniform; the compiler cannot tell after the capped waits)
           const uint32_t slot = __builtin_amdgcn_readfirstlane(ring0 + (p % S) * NIN * 1024);
           const unsigned row = (bq + i) * nq + q;
@@ -1568,7 +1565,8 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
       if (done) break;
       unsigned u;
       if (!direct) {
-        u = ring_flag_ld(&pitem[p % S]);
+        // claimed, and its bbase entry cannot be reused before this position is released
+        u = ring_flag_ld(&bbase[(p / B) % NB]) + p % B;
       } else {
         if (spins >= kRingSpinCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
         // the position's item from its batch's base once the batch is claimed;

@@ -96,15 +96,16 @@ int xor_blocks_cap() {
 // never beats both (profiles/r01_sequential_jobs.txt, cell-size sweeps). Sets
 // with smaller cells keep their stripes side by side in one launch (0).
 // Round 3, with the loader ring: GF stripes of <= 8 inputs over whole 16-B
-// vectors (RS(8+3) encode and rebuild) go two per launch, streamed through
-// one continuous ring (kJobsStreamed, codec_device.h gf_mac_stream): a block
-// that finishes its share of the first stripe goes straight on to the
-// second, so a pair pays one launch gap and one tail instead of two; +1.5 to
-// +2.5% on the RS(8+3) step against one launch per stripe. Streaming more
-// stripes per launch loses (4: +1%; all 11: -3.5%: blocks drift apart and
-// sweep different stripes at once); claiming the items at run time instead
-// (kJobsClaimed) keeps the blocks together, but costs the rebuild 3% more
-// than it gains the encode (profiles/r03_ab_stream.txt).
+// vectors (RS(8+3) encode and rebuild) run all in ONE launch whose blocks
+// claim their items at run time (kJobsClaimed, codec_device.h
+// gf_mac_claimed): one continuous loader ring per block over all the
+// stripes, the blocks of each XCD sweeping its rows together, so no launch
+// gaps, one tail per set instead of per stripe, and no drift between blocks:
+// +3.5% on the RS(8+3) step against one launch per stripe, +1.5% against
+// streamed pairs. Streamed (kJobsStreamed, static items) pays off only in
+// pairs (+1.5..2.5%): with more stripes per launch the blocks drift apart
+// and sweep different stripes at once (all 11: -3.5%); it stays the order of
+// XOR A/B runs (profiles/r03_ab_stream.txt).
 // REDSET_HIP_SEQUENTIAL=0..4 forces an order (A/B, tests; XOR launches take
 // 1 for 3 and 4); REDSET_HIP_STREAM_JOBS sets the stripes per streamed or
 // claimed launch (0 = all). Read at every plan build.
@@ -116,7 +117,8 @@ constexpr size_t kSequentialMinCell = 24u << 20;
 int sequential_jobs(int njobs, size_t nbytes, bool can_stream, bool can_claim, bool stream_default) {
   if (njobs < 2) return 0;
   int order = nbytes >= kSequentialMinCell
-                  ? (can_stream && stream_default ? redset_hip::kJobsStreamed : redset_hip::kJobsInLaunches)
+                  ? (can_claim ? redset_hip::kJobsClaimed
+                               : can_stream && stream_default ? redset_hip::kJobsStreamed : redset_hip::kJobsInLaunches)
                   : 0;
   const char* s = std::getenv("REDSET_HIP_SEQUENTIAL");
   if (s && s[0] >= '0' && s[0] <= '4' && s[1] == '\0') order = s[0] - '0';
@@ -131,7 +133,7 @@ int sequential_jobs(int njobs, size_t nbytes, bool can_stream, bool can_claim, b
 int stripes_per_launch(int order) {
   if (order == redset_hip::kJobsStreamed || order == redset_hip::kJobsClaimed) {
     const char* s = std::getenv("REDSET_HIP_STREAM_JOBS");
-    return (s && s[0] >= '0' && s[0] <= '9') ? std::atoi(s) : 2;
+    return (s && s[0] >= '0' && s[0] <= '9') ? std::atoi(s) : order == redset_hip::kJobsClaimed ? 0 : 2;
   }
   const char* s = std::getenv("REDSET_HIP_STRIPES_PER_LAUNCH");
   return (s && std::atoi(s) > 0) ? std::atoi(s) : 1;

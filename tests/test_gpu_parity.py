@@ -262,9 +262,9 @@ def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     one launch per stripe (=1, the default for cells >= 24 MiB but RS(8+3)'s; or
     per REDSET_HIP_STRIPES_PER_LAUNCH stripes), one launch whose blocks sweep the
     stripes in turn (=2), `group` stripes per launch streamed through one
-    continuous ring (=3, RS(8+3)'s default: 2; REDSET_HIP_STREAM_JOBS, 0 = all)
-    or the same with the items claimed at run time (=4; XOR plans take =1
-    there): same bytes."""
+    continuous ring (=3; REDSET_HIP_STREAM_JOBS, 0 = all) or the same with the
+    items claimed at run time (=4, RS(8+3)'s default, all stripes in one
+    launch; XOR plans take =1 there): same bytes."""
     monkeypatch.setenv("REDSET_HIP_SEQUENTIAL", mode)
     monkeypatch.setenv("REDSET_HIP_STRIPES_PER_LAUNCH", group)
     monkeypatch.setenv("REDSET_HIP_STREAM_JOBS", group)

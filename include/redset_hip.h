@@ -120,11 +120,10 @@ int redset_hip_xor_plan_rebuild(int ranks, int root, unsigned char* const* lofi,
                                 redset_hip_plan** out);
 
 /* Enqueue the plan's kernels on `stream`; no host synchronisation, no
- * allocation (safe inside hipStreamBeginCapture). Big-cell RS(8+3)-shaped
- * plans stream two stripes per launch; a plan forced to the
- * claimed order (REDSET_HIP_SEQUENTIAL=4, an A/B knob) keeps run-time claim
- * counters in the plan, so one plan must not execute on two streams at once
- * (an execute's outputs would race anyway). */
+ * allocation (safe inside hipStreamBeginCapture). A big-cell RS(8+3)
+ * encode plan runs as one launch whose blocks claim their rows at run time
+ * (DESIGN.md §4), with the claim counters in the plan: one plan must not
+ * execute on two streams at once (its outputs would race anyway). */
 int redset_hip_plan_execute(const redset_hip_plan* plan, void* stream);
 int redset_hip_plan_get_info(const redset_hip_plan* plan, redset_hip_plan_info* info);
 void redset_hip_plan_destroy(redset_hip_plan* plan);

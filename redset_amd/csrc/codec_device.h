@@ -1458,14 +1458,11 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
         // rows of this batch: (bq + i) * nq + q (RQ is a multiple of B, so a
         // batch stays in one job; one division per batch)
         const unsigned bq = base - bj * RQ;
-        // are the batch's B slots free already? (one LDS round trip for the
-        // batch instead of one per item; FREE words only grow)
-        bool all_free = true;
-#pragma unroll
-        for (unsigned i = 0; i < B; ++i) all_free &= ring_flag_ld(&freed[(p + i) % S]) >= (p + i) / S;
+        // (checking a batch's B slots at once, one LDS round trip instead of
+        // B, measured -1% on the encode: r03s46)
         for (unsigned i = 0; i < B; ++i, ++p) {
           const unsigned use = p / S;
-          if (!all_free && ring_flag_ld(&freed[p % S]) < use) {
+          if (ring_flag_ld(&freed[p % S]) < use) {
 #if REDSET_RING_DRAIN
             ring_wait_vm<0>();
             while (pub < p) publish();

@@ -113,12 +113,15 @@ constexpr size_t kSequentialMinCell = 24u << 20;
 
 // can_stream: the kernel has a streamed path for these jobs (GF: <= 8
 // inputs, XOR: <= 8 inputs, both over whole 16-B vectors); can_claim: a
-// claimed one (GF only); stream_default: streamed pairs are the default.
-int sequential_jobs(int njobs, size_t nbytes, bool can_stream, bool can_claim, bool stream_default) {
+// claimed one (GF only); claim_default / stream_default: which is the
+// default for big cells.
+int sequential_jobs(int njobs, size_t nbytes, bool can_stream, bool can_claim, bool claim_default,
+                     bool stream_default) {
   if (njobs < 2) return 0;
   int order = nbytes >= kSequentialMinCell
-                  ? (can_claim ? redset_hip::kJobsClaimed
-                               : can_stream && stream_default ? redset_hip::kJobsStreamed : redset_hip::kJobsInLaunches)
+                  ? (can_claim && claim_default ? redset_hip::kJobsClaimed
+                     : can_stream && stream_default ? redset_hip::kJobsStreamed
+                                                    : redset_hip::kJobsInLaunches)
                   : 0;
   const char* s = std::getenv("REDSET_HIP_SEQUENTIAL");
   if (s && s[0] >= '0' && s[0] <= '4' && s[1] == '\0') order = s[0] - '0';
@@ -266,7 +269,11 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     G.bytes_only = P.bytes_only;
     G.nbytes = nbytes;
     const bool whole = P.nin <= 8 && !P.bytes_only && nbytes % 16 == 0;
-    G.sequential = sequential_jobs(G.njobs, nbytes, whole, whole, true);
+    // claimed items for 3-4 outputs (the RS(8+3) encode: 6.45-6.47 TB/s against
+    // 6.22-6.27 streamed in pairs on two boxes); pairs for 1-2 (the rebuild:
+    // 6.35-6.41 against 5.99-6.33 claimed; its lighter consumers leave the
+    // loader, whose per-item cost the claimed order raises, setting the pace)
+    G.sequential = sequential_jobs(G.njobs, nbytes, whole, whole, P.nout >= 3, true);
     G.group = stripes_per_launch(G.sequential);
     G.blocks_per_job = blocks_per_job(jobs_sharing_grid(G.sequential, G.njobs, G.group), nbytes,
                                       redset_hip::gf_blocks_per_cu(P.nin));
@@ -284,7 +291,7 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     X.bytes_only = P.bytes_only;
     X.nbytes = nbytes;
     const bool whole = P.nin <= 8 && !P.bytes_only && nbytes % 16 == 0;
-    X.sequential = sequential_jobs(X.njobs, nbytes, whole, false, xor_stream_default());
+    X.sequential = sequential_jobs(X.njobs, nbytes, whole, false, false, xor_stream_default());
     X.group = stripes_per_launch(X.sequential);
     X.blocks_per_job = blocks_per_job(jobs_sharing_grid(X.sequential, X.njobs, X.group), nbytes, xor_blocks_cap());
     xall.insert(xall.end(), P.jobs.begin(), P.jobs.end());

@@ -738,6 +738,20 @@ typedef __attribute__((address_space(3))) v4u lr_u4;
 typedef __attribute__((address_space(3))) volatile unsigned lr_flag;  // LDS, never flat
 __device__ __forceinline__ unsigned ring_flag_ld(unsigned* p) { return *(lr_flag*) p; }
 __device__ __forceinline__ void ring_flag_st(unsigned* p, unsigned v) { *(lr_flag*) p = v; }
+// A loader publishes an item: lane 0 writes its FULL word (0), or (A/B knob
+// REDSET_RING_PUBLISH_ALL=1) every lane writes the same value, which spares the
+// exec-mask juggling of a one-lane write
+#ifndef REDSET_RING_PUBLISH_ALL
+#define REDSET_RING_PUBLISH_ALL 0
+#endif
+__device__ __forceinline__ void ring_publish(unsigned* p, unsigned v, int lane) {
+#if REDSET_RING_PUBLISH_ALL
+  (void) lane;
+  ring_flag_st(p, v);
+#else
+  if (lane == 0) ring_flag_st(p, v);
+#endif
+}
 template <int N>
 __device__ __forceinline__ void ring_wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -801,7 +815,7 @@ __device__ __forceinline__ void ring_sweep(v4u* ring, g_cu4* const (&in)[NIN], s
     // items [pub, k) are issued and not yet published
     size_t pub = 0;
     auto publish = [&]() {
-      if (lane == 0) ring_flag_st(&full[pub % S], static_cast<unsigned>(pub / S) + 1);
+      ring_publish(&full[pub % S], static_cast<unsigned>(pub / S) + 1, lane);
       ++pub;
     };
     for (size_t k = 0; k < K; ++k) {
@@ -1120,7 +1134,7 @@ __device__ __forceinline__ void gf_mac_stream(const GfLaunch& L) {
     const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lr_u4*) ring)));
     unsigned pub = 0;  // items [pub, g) are issued and not yet published
     auto publish = [&]() {
-      if (lane == 0) ring_flag_st(&full[pub % S], pub / S + 1);
+      ring_publish(&full[pub % S], pub / S + 1, lane);
       ++pub;
     };
     // every consumer's next item is >= T (all items before T are done)
@@ -1400,7 +1414,7 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
       const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lr_u4*) ring)));
       unsigned pub = 0;
       auto publish = [&]() {
-        if (lane == 0) ring_flag_st(&full[pub % S], pub / S + 1);
+        ring_publish(&full[pub % S], pub / S + 1, lane);
         ++pub;
       };
       auto past = [&](unsigned T) {
@@ -1713,7 +1727,7 @@ __device__ __forceinline__ void xor_stream(const XorLaunch& L) {
     const uint32_t ring0 = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(reinterpret_cast<uintptr_t>((lr_u4*) ring)));
     unsigned pub = 0;
     auto publish = [&]() {
-      if (lane == 0) ring_flag_st(&full[pub % S], pub / S + 1);
+      ring_publish(&full[pub % S], pub / S + 1, lane);
       ++pub;
     };
     const uint8_t* in[NIN];

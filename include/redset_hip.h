@@ -371,6 +371,12 @@ void redset_hip_rccl_transport_destroy(redset_hip_rccl* handle);
  * Synchronises the device; `clear` resets the count. */
 int redset_hip_ring_faults(unsigned* count, int clear);
 
+/* 1 if this is the test twin library (built with REDSET_HIP_TEST_KNOBS: it
+ * honours the environment knobs the test suite uses to force job orders,
+ * ring fallbacks and injected failures), 0 for the product library, which
+ * reads none of them. */
+int redset_hip_test_build(void);
+
 /* Text of the last failure on this thread ("" if none). */
 const char* redset_hip_last_error(void);
 /* For layers built on this library (the per-rank backends of

@@ -62,9 +62,13 @@ void redset_hip_rank_scratch_release(void);
  * point-to-point: MPI_Isend / MPI_Irecv of every message of an exchange,
  * then MPI_Waitall -- the reference's own primitives (src/redset_reedsolomon.c:
  * 690-694, :713-733) for builds without RCCL or across nodes. Buffers are
- * host memory (device_buffers = 0), or device memory staged through pinned
- * host buffers with hipMemcpyAsync (device_buffers = 1; no GPU-aware MPI
- * needed). Messages above 1 GiB are split alike on both sides. */
+ * host memory (device_buffers = 0; the exchange waits for `stream` only if
+ * one is passed, and a host-only caller needs no HIP runtime), device memory
+ * staged through pinned host buffers with hipMemcpyAsync (device_buffers = 1;
+ * no GPU-aware MPI needed), or page-locked host memory that HIP kernels read
+ * and write in place (device_buffers = 2: every exchange first waits for
+ * `stream`, the null stream included). Messages above 1 GiB are split alike
+ * on both sides. */
 typedef struct redset_hip_mpi_transport redset_hip_mpi_transport;
 int redset_hip_mpi_transport_create(MPI_Comm comm, int device_buffers, redset_hip_transport* out,
                                     redset_hip_mpi_transport** handle);

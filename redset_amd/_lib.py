@@ -11,7 +11,8 @@ import ctypes
 import os
 from ctypes import POINTER, c_char_p, c_int, c_size_t, c_ubyte, c_uint, c_ulonglong, c_void_p
 
-# REDSET_HIP_LIBRARY points at another build of the same library (A/B runs)
+# REDSET_HIP_LIBRARY points at another build of the same library (the test
+# twin redset_amd/lib_test/, whose planner honours the test knobs)
 LIB_PATH = os.environ.get("REDSET_HIP_LIBRARY") or os.path.join(
     os.path.dirname(os.path.abspath(__file__)), "lib", "libredset_hip.so")
 
@@ -43,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "redset_hip_xor_combine",
     "redset_hip_rs_decode_matrix",
     "redset_hip_ring_faults",
+    "redset_hip_test_build",
     "redset_hip_last_error",
     "redset_hip_record_error",
     "redset_hip_version",
@@ -221,6 +223,7 @@ _SIGNATURES = {
     "redset_hip_rccl_transport_create": (c_int, [POINTER(c_ubyte), c_int, c_int, POINTER(Transport), POINTER(c_void_p)]),
     "redset_hip_rccl_transport_destroy": (None, [c_void_p]),
     "redset_hip_ring_faults": (c_int, [POINTER(c_uint), c_int]),
+    "redset_hip_test_build": (c_int, []),
     "redset_hip_last_error": (c_char_p, []),
     "redset_hip_record_error": (c_int, [c_char_p]),
     "redset_hip_version": (c_char_p, []),

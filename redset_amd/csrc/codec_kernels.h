@@ -2,6 +2,14 @@
 // (codec_kernels.hip) and the host planner (redset_hip.cpp).
 #pragma once
 
+// REDSET_HIP_TEST_KNOBS=1 builds the test twin library (redset_amd/lib_test):
+// its planner and launchers honour the REDSET_HIP_* / REDSET_HIP_TEST_*
+// environment knobs the test suite uses to force job orders, ring fallbacks
+// and injected failures. The product library reads none of them.
+#ifndef REDSET_HIP_TEST_KNOBS
+#define REDSET_HIP_TEST_KNOBS 0
+#endif
+
 #include <cstddef>
 #include <cstdint>
 
@@ -29,12 +37,12 @@ constexpr int kJobsStreamed = 3;
 // items in batches from a shared per-XCD queue (GfLaunch::claim), so no block
 // runs ahead of the others or idles at the end (codec_device.h gf_mac_claimed).
 constexpr int kJobsClaimed = 4;
-// claim queues: one counter per XCD, 128 B apart, then the finished-block
-// counter (kClaimWords words per launch, zeroed by the planner; the last
-// block of a launch zeroes them again)
+// claim queues: one counter per XCD, 128 B apart (kClaimWords words per
+// launch, plan-owned; the launcher zeroes them on the launch's stream before
+// every claimed launch, so no state carries from one launch to the next)
 constexpr int kClaimQueues = 8;
 constexpr int kClaimStride = 32;
-constexpr int kClaimWords = (kClaimQueues + 1) * kClaimStride;
+constexpr int kClaimWords = kClaimQueues * kClaimStride;
 
 // One stripe (or one pass over a slice of a stripe's members):
 // out[j] (^)= sum_i coef[j][i] * in[i] over GF(2^8), byte by byte.
@@ -59,7 +67,9 @@ struct GfLaunch {
                             // kJobsStreamed / kJobsClaimed: jobs per launch, in turn (0 = all)
   size_t nbytes;            // bytes per cell
   unsigned* fault;          // set by the launcher: counts capped ring spins (codec_device.h)
-  unsigned* claim;          // kJobsClaimed: kClaimWords zeroed device words (planner)
+  unsigned* claim;          // kJobsClaimed: kClaimWords device words (plan; zeroed per launch)
+  unsigned spin_cap;        // set by the launcher; read by test builds only (codec_device.h kRingSpinCap)
+  unsigned claim_delay;     // test builds: s_sleep rounds the claimer waits between claiming and recording
 };
 
 // XOR of `nin` inputs into one output (the XOR scheme's parity / rebuild).
@@ -80,6 +90,7 @@ struct XorLaunch {
   int group;
   size_t nbytes;
   unsigned* fault;          // set by the launcher (see GfLaunch)
+  unsigned spin_cap;        // (see GfLaunch)
 };
 
 // launchers (codec_kernels.hip); return hipError_t as int
@@ -96,24 +107,15 @@ int device_cu_count();
 int read_ring_faults(unsigned* count, int clear);
 // occupancy of the GF kernel for a given input count (blocks per CU)
 int gf_blocks_per_cu(int nin);
+// 1 in the test twin library (built with REDSET_HIP_TEST_KNOBS), else 0
+int test_knobs();
 
-// Sweep of the kernels (codec_device.h): REDSET_RING = 1 streams the
-// inputs through a loader-wave LDS-DMA ring (ring_sweep; items in flight per
-// ring_depth), 0 = the plain per-wave sweep.
-#ifndef REDSET_RING
-#define REDSET_RING 1
-#endif
-// Threads per block, one block per CU: the ring runs 1 loader + 15 consumer
-// waves (1024), the plain sweep 8 waves (512). A/B in profiles/r02_ab_ring.txt,
-// r02_ab_block_waves.txt.
-#ifndef REDSET_BLOCK
-#if REDSET_RING
-#define REDSET_BLOCK 1024
-#else
-#define REDSET_BLOCK 512
-#endif
-#endif
-constexpr int kBlock = REDSET_BLOCK;
+// Threads per block, one block per CU: the kernels stream their inputs
+// through a loader-wave LDS-DMA ring (codec_device.h ring_sweep) run by 1
+// loader + 15 consumer waves. 7 or 11 consumers cannot keep up with the GF
+// math; the per-wave sweep this replaced ran 8 waves of 512 threads
+// (profiles/r02_ab_ring.txt, r02_ab_block_waves.txt).
+constexpr int kBlock = 1024;
 
 // The kernels of one input count: [nout - 1][accumulate] for gf_mac,
 // [accumulate] for xor_reduce; *_arg take the job by value.

@@ -4,6 +4,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <cstdlib>
 
 #include "codec_kernels.h"
 
@@ -43,14 +44,7 @@ int jobs_per_launch(const Launch& L) {
 // from several threads (the pipeline's compute thread, per-rank backends,
 // callers), so the per-device address cache is atomic; a racing first
 // lookup resolves the same address twice, which is harmless.
-#if REDSET_BLOCK_CLOCK
-// timing-only builds: the fault word, then 3 words of 64 bits per block
-// (codec_device.h BlockClock)
-constexpr int kClockBlocks = 4096;
-__device__ unsigned g_ring_fault[64 + 6 * kClockBlocks];
-#else
 __device__ unsigned g_ring_fault;
-#endif
 
 unsigned* ring_fault_word() {
   static std::atomic<unsigned*> addr[64];
@@ -66,7 +60,39 @@ unsigned* ring_fault_word() {
   }
   return a;
 }
+// Test builds (REDSET_HIP_TEST_KNOBS, the twin library of the test suite):
+// the loader ring's poll cap and a claimer delay from the environment
+// (REDSET_HIP_TEST_SPIN_CAP, REDSET_HIP_TEST_CLAIM_DELAY), so the suite can
+// drive the ring's fallbacks and the claimed kernel's claim/record window on
+// every launch. The product library reads no environment here.
+unsigned spin_cap() {
+#if REDSET_HIP_TEST_KNOBS
+  static const unsigned cap = [] {
+    const char* s = std::getenv("REDSET_HIP_TEST_SPIN_CAP");
+    const long v = s ? std::atol(s) : 0;
+    return v > 0 ? static_cast<unsigned>(v) : 1u << 24;
+  }();
+  return cap;
+#else
+  return 1u << 24;
+#endif
+}
+
+unsigned claim_delay() {
+#if REDSET_HIP_TEST_KNOBS
+  static const unsigned d = [] {
+    const char* s = std::getenv("REDSET_HIP_TEST_CLAIM_DELAY");
+    const long v = s ? std::atol(s) : 0;
+    return v > 0 ? static_cast<unsigned>(v) : 0u;
+  }();
+  return d;
+#else
+  return 0;
+#endif
+}
 }  // namespace
+
+int test_knobs() { return REDSET_HIP_TEST_KNOBS ? 1 : 0; }
 
 int read_ring_faults(unsigned* count, int clear) {
   unsigned v = 0;
@@ -79,17 +105,6 @@ int read_ring_faults(unsigned* count, int clear) {
   return e;
 }
 
-#if REDSET_BLOCK_CLOCK
-}  // namespace redset_hip
-// timing-only builds: (start, end, XCC_ID << 32 | HW_ID) of blocks [0, n) of
-// the last gf_mac / xor launch
-extern "C" int redset_hip_debug_block_clock(unsigned long long* out, int n) {
-  if (n > redset_hip::kClockBlocks) n = redset_hip::kClockBlocks;
-  return hipMemcpyFromSymbol(out, HIP_SYMBOL(redset_hip::g_ring_fault), 3 * sizeof(unsigned long long) * n,
-                             64 * sizeof(unsigned), hipMemcpyDeviceToHost);
-}
-namespace redset_hip {
-#endif
 
 int device_cu_count() {
   static int cus = 0;
@@ -129,7 +144,15 @@ int launch_gf(const GfLaunch& L, void* stream) {
     GfLaunch one = L;
     one.job0 = j;
     one.fault = ring_fault_word();
+    one.spin_cap = spin_cap();
+    one.claim_delay = claim_delay();
     if (L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) one.njobs = std::min(per, L.njobs - j);
+    if (L.sequential == kJobsClaimed && L.claim) {
+      // the claim queues start at zero for every launch, whatever an earlier
+      // launch left (aborted, replayed from a graph, another stream's)
+      const hipError_t e = hipMemsetAsync(L.claim, 0, kClaimWords * sizeof(unsigned), static_cast<hipStream_t>(stream));
+      if (e != hipSuccess) return e;
+    }
     const int n = (L.sequential == kJobsInKernel || L.sequential == kJobsStreamed || L.sequential == kJobsClaimed)
                       ? 1
                       : std::min(per, L.njobs - j);
@@ -146,6 +169,7 @@ int launch_gf_single(const GfLaunch& L, const GfJob& J, void* stream) {
   if (L.nbytes == 0) return hipSuccess;
   GfLaunch one = L;
   one.fault = ring_fault_word();
+  one.spin_cap = spin_cap();
   hipLaunchKernelGGL(kernel_set(L.nin).gf_arg[L.nout - 1][L.accumulate ? 1 : 0], dim3(static_cast<unsigned>(L.blocks_per_job)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), one, J);
   return hipGetLastError();
@@ -156,6 +180,7 @@ int launch_xor_single(const XorLaunch& L, const XorJob& J, void* stream) {
   if (L.nbytes == 0) return hipSuccess;
   XorLaunch one = L;
   one.fault = ring_fault_word();
+  one.spin_cap = spin_cap();
   hipLaunchKernelGGL(kernel_set(L.nin).xr_arg[L.accumulate ? 1 : 0], dim3(static_cast<unsigned>(L.blocks_per_job)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), one, J);
   return hipGetLastError();
@@ -170,6 +195,7 @@ int launch_xor(const XorLaunch& L, void* stream) {
     XorLaunch one = L;
     one.job0 = j;
     one.fault = ring_fault_word();
+    one.spin_cap = spin_cap();
     if (L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) one.njobs = std::min(per, L.njobs - j);
     const int n = (L.sequential == kJobsInKernel || L.sequential == kJobsStreamed || L.sequential == kJobsClaimed)
                       ? 1

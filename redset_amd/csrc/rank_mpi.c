@@ -235,10 +235,16 @@ static int agree_setup(MPI_Comm comm, int rc) {
   return 0;
 }
 
-/* Test hook: REDSET_HIP_INJECT_DEVICE_FAILURE=<rank> makes that rank's first
- * device step report a failure (tests/mpi/rank_test.c drives it), so the
- * keep-the-collective-going path below is exercised without a broken GPU. */
+/* Test builds only (-DREDSET_HIP_TEST_KNOBS, the twin library the test suite
+ * loads for it): REDSET_HIP_INJECT_DEVICE_FAILURE=<rank> makes that rank's
+ * first device step report a failure (tests/mpi/rank_test.c drives it), so
+ * the keep-the-collective-going path below is exercised without a broken
+ * GPU. The product library reads no such variable. */
+#ifndef REDSET_HIP_TEST_KNOBS
+#define REDSET_HIP_TEST_KNOBS 0
+#endif
 static int injected_device_failure(MPI_Comm comm) {
+  if (!REDSET_HIP_TEST_KNOBS) return 0;
   static int fired = 0;
   const char* v = getenv("REDSET_HIP_INJECT_DEVICE_FAILURE");
   int r = -1;
@@ -823,6 +829,7 @@ out:
 struct redset_hip_mpi_transport {
   MPI_Comm comm;
   int world, rank, device;
+  int hip_host;     /* host buffers that HIP kernels on `stream` read and write */
   uint8_t* stage;   /* pinned staging (device mode) */
   size_t stage_len;
   MPI_Request* req;
@@ -850,8 +857,10 @@ static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream
   }
   /* work already on the stream produced the send buffers -- in host mode
    * too, where a HIP compute over page-locked slabs may still be writing
-   * them (a host-only caller passes no stream and needs no HIP runtime) */
-  if ((T->device || s) && hipStreamSynchronize(s) != hipSuccess) return fail("mpi transport: stream sync failed");
+   * them, on the null stream as well (device_buffers = 2); a host-only
+   * caller (device_buffers = 0, no stream) needs no HIP runtime */
+  if ((T->device || T->hip_host || s) && hipStreamSynchronize(s) != hipSuccess)
+    return fail("mpi transport: stream sync failed");
   if ((int) nreq > T->req_cap) {
     MPI_Request* r = realloc(T->req, sizeof(*r) * nreq);
     if (!r) return fail("out of host memory");
@@ -921,7 +930,12 @@ int redset_hip_mpi_transport_create(MPI_Comm comm, int device_buffers, redset_hi
     return REDSET_FAILURE;
   }
   T->comm = comm;
-  T->device = device_buffers != 0;
+  if (device_buffers < 0 || device_buffers > 2) {
+    free(T);
+    return fail("mpi_transport_create: device_buffers %d is not 0, 1 or 2", device_buffers);
+  }
+  T->device = device_buffers == 1;
+  T->hip_host = device_buffers == 2;
   out->world = T->world;
   out->rank = T->rank;
   out->exchange = mpi_exchange;

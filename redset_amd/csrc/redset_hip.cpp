@@ -54,36 +54,28 @@ int hip_check(hipError_t e, const char* what) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
-// Resident blocks per CU the codec aims for: one block (the ring's 1024
-// threads = 1 loader + 15 consumer waves, or the plain sweep's 512 = 8
-// waves; codec_kernels.h). For the plain sweep 8 waves (64 KiB of loads in
-// flight) per CU beat 4, 12, 16 and 32 on every box measured
-// (tools/bpc_sweep.sh, profiles/r01_ab_pipeline.txt, r01_ab_waves_per_eu.txt);
-// the ring needs its block alone on the CU (128 KiB of LDS).
-// REDSET_HIP_BLOCKS_PER_CU overrides it.
-int target_blocks_per_cu(int occupancy) {
-  static int env = -1;
-  if (env < 0) {
-    const char* s = std::getenv("REDSET_HIP_BLOCKS_PER_CU");
-    env = (s && std::atoi(s) > 0) ? std::atoi(s) : 0;
-  }
-  const int want = env > 0 ? env : std::max(1, 512 / redset_hip::kBlock);  // 8 waves per CU
-  return std::max(1, std::min(want, occupancy));
+// Test builds only (REDSET_HIP_TEST_KNOBS, codec_kernels.h): an environment
+// override of a planning choice; the product library always takes `dflt`.
+// Read at every plan build.
+int test_knob(const char* name, int dflt) {
+#if REDSET_HIP_TEST_KNOBS
+  const char* s = std::getenv(name);
+  if (s && s[0] >= '0' && s[0] <= '9') return std::atoi(s);
+#else
+  (void) name;
+#endif
+  return dflt;
 }
 
-// Resident XOR blocks per CU: one. With the plain sweep, 256-thread blocks
-// one per CU (4 waves) ran the 7 read streams at 6.00 TB/s against 5.78 at
-// two (profiles/r01_ab_xor_blocks.txt) and 512-thread blocks (8 waves)
-// 5.98-6.00 (profiles/r01_ab_block_size.txt); the ring's block fills the
-// CU's LDS. REDSET_HIP_XOR_BLOCKS_PER_CU overrides it.
-int xor_blocks_cap() {
-  static int env = -1;
-  if (env < 0) {
-    const char* s = std::getenv("REDSET_HIP_XOR_BLOCKS_PER_CU");
-    env = (s && std::atoi(s) > 0) ? std::atoi(s) : 1;
-  }
-  return env;
-}
+// Resident blocks per CU the codec aims for: one block of the ring's 1024
+// threads (1 loader + 15 consumer waves, codec_kernels.h), alone on the CU
+// (it takes 146 KiB of LDS).
+int target_blocks_per_cu(int occupancy) { return std::max(1, std::min(1, occupancy)); }
+
+// Resident XOR blocks per CU: one, as for gf_mac (the ring's block fills the
+// CU's LDS; with the per-wave sweep before it, one 256-thread block per CU
+// also beat two, profiles/r01_ab_xor_blocks.txt).
+int xor_blocks_cap() { return 1; }
 
 // Job order of a plan's launches (codec_kernels.h). Stripes in sequence, one
 // launch each over the whole grid (kJobsInLaunches), keep one stripe's ~11
@@ -106,9 +98,10 @@ int xor_blocks_cap() {
 // pairs (+1.5..2.5%): with more stripes per launch the blocks drift apart
 // and sweep different stripes at once (all 11: -3.5%); it stays the order of
 // XOR A/B runs (profiles/r03_ab_stream.txt).
-// REDSET_HIP_SEQUENTIAL=0..4 forces an order (A/B, tests; XOR launches take
-// 1 for 3 and 4); REDSET_HIP_STREAM_JOBS sets the stripes per streamed or
-// claimed launch (0 = all). Read at every plan build.
+// Test builds: REDSET_HIP_SEQUENTIAL=0..4 forces an order (XOR launches take
+// 1 for 4); REDSET_HIP_STREAM_JOBS sets the stripes per streamed or claimed
+// launch (0 = all), REDSET_HIP_STRIPES_PER_LAUNCH those side by side per
+// launch in sequence mode.
 constexpr size_t kSequentialMinCell = 24u << 20;
 
 // can_stream: the kernel has a streamed path for these jobs (GF: <= 8
@@ -123,33 +116,27 @@ int sequential_jobs(int njobs, size_t nbytes, bool can_stream, bool can_claim, b
                      : can_stream && stream_default ? redset_hip::kJobsStreamed
                                                     : redset_hip::kJobsInLaunches)
                   : 0;
-  const char* s = std::getenv("REDSET_HIP_SEQUENTIAL");
-  if (s && s[0] >= '0' && s[0] <= '4' && s[1] == '\0') order = s[0] - '0';
+  const int forced = test_knob("REDSET_HIP_SEQUENTIAL", -1);
+  if (forced >= 0 && forced <= 4) order = forced;
   if ((order == redset_hip::kJobsStreamed && !can_stream) || (order == redset_hip::kJobsClaimed && !can_claim))
     order = redset_hip::kJobsInLaunches;
   return order;
 }
 
 // Stripes per launch: in sequence mode side by side within the launch
-// (REDSET_HIP_STRIPES_PER_LAUNCH, default 1); streamed or claimed, one after
-// another through the ring (REDSET_HIP_STREAM_JOBS, default 2, 0 = all).
+// (default 1); streamed, two stripes one after another through the ring;
+// claimed, the whole set in one launch (0 = all).
 int stripes_per_launch(int order) {
-  if (order == redset_hip::kJobsStreamed || order == redset_hip::kJobsClaimed) {
-    const char* s = std::getenv("REDSET_HIP_STREAM_JOBS");
-    return (s && s[0] >= '0' && s[0] <= '9') ? std::atoi(s) : order == redset_hip::kJobsClaimed ? 0 : 2;
-  }
-  const char* s = std::getenv("REDSET_HIP_STRIPES_PER_LAUNCH");
-  return (s && std::atoi(s) > 0) ? std::atoi(s) : 1;
+  if (order == redset_hip::kJobsStreamed || order == redset_hip::kJobsClaimed)
+    return test_knob("REDSET_HIP_STREAM_JOBS", order == redset_hip::kJobsClaimed ? 0 : 2);
+  return std::max(1, test_knob("REDSET_HIP_STRIPES_PER_LAUNCH", 1));
 }
 
 // XOR plans keep a launch per stripe: streamed pairs (xor_stream) measured
 // within the XOR leg's run-to-run spread, 6.26 against 6.30 TB/s over three
-// alternating pairs (profiles/r03_ab_stream.txt). A/B knob:
+// alternating pairs (profiles/r03_ab_stream.txt). Test builds:
 // REDSET_HIP_XOR_STREAM=1 streams them in pairs.
-bool xor_stream_default() {
-  const char* s = std::getenv("REDSET_HIP_XOR_STREAM");
-  return s && s[0] == '1';
-}
+bool xor_stream_default() { return test_knob("REDSET_HIP_XOR_STREAM", 0) == 1; }
 
 int launches_of(int order, int njobs, int group) {
   if (order == redset_hip::kJobsStreamed || order == redset_hip::kJobsClaimed)
@@ -422,6 +409,8 @@ int run_stripe(const StripeMap& m, const uint8_t* const* in, uint8_t* const* out
 }  // namespace redset_hip
 
 extern "C" {
+
+int redset_hip_test_build(void) { return redset_hip::test_knobs(); }
 
 int redset_hip_ring_faults(unsigned* count, int clear) {
   if (!count) return fail("ring_faults: null argument");

@@ -251,12 +251,16 @@ int hip_ok(hipError_t e, const char* what) { return e == hipSuccess ? 0 : fail("
 // MI355X (tools/zerocopy_probe.py): a kernel's host reads run at the SDMA
 // H2D rate (55-56 GB/s) while its host writes use the other direction at the
 // same time, 75.5 GB/s of PCIe bytes for an 8-in / 3-out stripe against the
-// staged pipeline's ~60. REDSET_HIP_ZERO_COPY=0 forces the staged pipeline.
+// staged pipeline's ~60. Test builds (REDSET_HIP_TEST_KNOBS):
+// REDSET_HIP_ZERO_COPY=0 forces the staged pipeline over mapped cells.
 // Returns 1 (not applicable) without side effects when a cell is not mapped.
 int try_zero_copy(const std::vector<StripeMap>& maps, size_t chunk, const redset_hip_io* io,
                   redset_hip_stream_stats* st, int* rc_out) {
+#if REDSET_HIP_TEST_KNOBS
   const char* env = std::getenv("REDSET_HIP_ZERO_COPY");
-  if ((env && env[0] == '0') || !io->map || chunk == 0) return 1;
+  if (env && env[0] == '0') return 1;
+#endif
+  if (!io->map || chunk == 0) return 1;
   std::vector<std::vector<const uint8_t*>> ins(maps.size());
   std::vector<std::vector<uint8_t*>> outs(maps.size());
   auto dev = [&](const CellRef& c) -> void* {

@@ -14,6 +14,34 @@ if TESTS not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP device); run with -m gpu")
     config.addinivalue_line("markers", "slow: long-running")
+    config.addinivalue_line(
+        "markers", "knobs: drives the test twin library's environment knobs (redset_amd/lib_test); "
+        "collected only when that library is the one loaded (tests/test_gpu_test_build.py runs them)")
+
+
+TEST_LIB_DIR = os.path.join(ROOT, "redset_amd", "lib_test")
+
+
+def test_build_loaded() -> bool:
+    """The codec library this process loads is the test twin (built with
+    REDSET_HIP_TEST_KNOBS): asked of the library itself."""
+    try:
+        import redset_amd._lib as L
+
+        return bool(L.load().redset_hip_test_build())
+    except Exception:
+        return False
+
+
+def pytest_collection_modifyitems(config, items):
+    """Tests marked `knobs` set the environment knobs only the test twin
+    library honours (the product library reads none): run them only when the
+    twin is loaded, deselected (not skipped) otherwise."""
+    knob_items = [it for it in items if it.get_closest_marker("knobs") is not None]
+    if not knob_items or test_build_loaded():
+        return
+    config.hook.pytest_deselected(items=knob_items)
+    items[:] = [it for it in items if it.get_closest_marker("knobs") is None]
 
 
 def gpu_available() -> bool:
@@ -33,10 +61,10 @@ def oracle():
     return oracle_lib
 
 
-# REDSET_RING_FALLBACK_RUN=1: the suite runs against the spin-cap twin of the
-# library (tests/test_gpu_ring_fallback.py), whose ring handshakes give up on
-# purpose; capped spins are then expected, counted and written to
-# REDSET_RING_FAULT_LOG instead of failing the test.
+# REDSET_RING_FALLBACK_RUN=1: the suite runs against the test twin of the
+# library with a 4-poll ring cap (tests/test_gpu_test_build.py), whose ring
+# handshakes give up on purpose; capped spins are then expected, counted and
+# written to REDSET_RING_FAULT_LOG instead of failing the test.
 FALLBACK_RUN = os.environ.get("REDSET_RING_FALLBACK_RUN") == "1"
 _fallback_faults = [0]
 

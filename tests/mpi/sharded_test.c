@@ -7,7 +7,7 @@
  * slicing and both exchanges are checked against the oracle's whole-set
  * encode / rebuild without a GPU.
  *
- * usage: sharded_test [--gpu | --gpu-host] <p> <e> <chunk> [lost ranks...]   (world = MPI size)
+ * usage: sharded_test [--gpu | --gpu-host | --gpu-host-null] <p> <e> <chunk> [lost ranks...]   (world = MPI size)
  * SHARDED_TEST_REPS=<n> (--gpu): after the checks, time n rebuilds with the
  * pipelined execute and n with the three phases one after another (slowest
  * process, ms per rebuild).
@@ -18,6 +18,9 @@
  * HIP gf_mac plans reading and writing them in place, and the MPI transport
  * works on the host buffers directly -- it must wait for the kernels that
  * wrote a return exchange's slices before it sends them.
+ * --gpu-host-null: the same on the null stream (the transport is
+ * created for HIP-written host buffers, device_buffers = 2, and must wait for
+ * the null stream too).
  * Placement: `world` sets of p members, member m on process (m * 7 + 3) %
  * world (SHARDED_TEST_SEED=<s>: on a pseudo-random process), hosted slots in
  * ascending member order. Exit 0 iff every process
@@ -92,7 +95,8 @@ int main(int argc, char** argv) {
   int world, me;
   MPI_Comm_size(MPI_COMM_WORLD, &world);
   MPI_Comm_rank(MPI_COMM_WORLD, &me);
-  const int host_slabs = argc > 1 && strcmp(argv[1], "--gpu-host") == 0;
+  const int null_stream = argc > 1 && strcmp(argv[1], "--gpu-host-null") == 0;
+  const int host_slabs = null_stream || (argc > 1 && strcmp(argv[1], "--gpu-host") == 0);
   const int gpu = host_slabs || (argc > 1 && strcmp(argv[1], "--gpu") == 0);
   HOST_SLABS = host_slabs;
   if (gpu) {
@@ -155,7 +159,8 @@ int main(int argc, char** argv) {
   if (host_slabs) {
     /* every slab page-locked; kernels and MPI use the same addresses */
     if (hipHostMalloc((void**) &dHD, hd, 0) || hipHostMalloc((void**) &dHP, hp, 0) ||
-        hipHostMalloc((void**) &dGD, hd, 0) || hipHostMalloc((void**) &dGP, hp, 0) || hipStreamCreate(&stream)) {
+        hipHostMalloc((void**) &dGD, hd, 0) || hipHostMalloc((void**) &dGP, hp, 0) ||
+        (!null_stream && hipStreamCreate(&stream))) {
       fprintf(stderr, "rank %d: pinned setup failed\n", me);
       MPI_Abort(MPI_COMM_WORLD, 3);
     }
@@ -181,7 +186,7 @@ int main(int argc, char** argv) {
   }
   redset_hip_sharded *enc = NULL, *reb = NULL;
   const redset_hip_compute* cp = gpu ? NULL : &comp;
-  int ok = redset_hip_rs_create(P, E, &rs) == 0 && redset_hip_mpi_transport_create(MPI_COMM_WORLD, gpu && !host_slabs, &tr, &th) == 0 &&
+  int ok = redset_hip_rs_create(P, E, &rs) == 0 && redset_hip_mpi_transport_create(MPI_COMM_WORLD, host_slabs ? 2 : gpu ? 1 : 0, &tr, &th) == 0 &&
            redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, &tr, cp, &enc) == 0 &&
            (missing == 0 ||
             redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, &tr, cp, &reb) == 0);

@@ -151,13 +151,19 @@ def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme
     else:
         args = [scheme, "encode", e, tmp, buf]
     cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST] + [str(a) for a in args]
-    res = run_group(cmd, 90, env={**os.environ, **env})
+    env = {**os.environ, **env}
+    if "REDSET_HIP_INJECT_DEVICE_FAILURE" in env:
+        # only the test twin honours the injection knob (the product reads no
+        # environment): the driver loads it ahead of its RUNPATH
+        twin = os.path.join(ROOT, "redset_amd", "lib_test")
+        env["LD_LIBRARY_PATH"] = twin + (":" + env["LD_LIBRARY_PATH"] if env.get("LD_LIBRARY_PATH") else "")
+    res = run_group(cmd, 90, env=env)
     assert res.returncode != 0, res.stdout + res.stderr  # every rank exits 1 (alltrue is false)
     assert "backend failed" in res.stderr
     assert "Sanitizer" not in res.stderr, res.stderr[-4000:]  # tools/gpu_asan.sh builds
 
 
-@pytest.mark.parametrize("mode", ["--gpu", "--gpu-host"])
+@pytest.mark.parametrize("mode", ["--gpu", "--gpu-host", "--gpu-host-null"])
 @pytest.mark.parametrize("np_,p,e,chunk,lost", [(2, 11, 3, 300_001, [1, 2]), (4, 20, 4, 65536, [0, 5, 19]),
                                                  (3, 6, 3, 1000, [2])])
 def test_mpi_sharded_gpu(np_, p, e, chunk, lost, mode):

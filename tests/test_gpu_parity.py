@@ -257,6 +257,7 @@ def test_xor_encode_and_rebuild(rd, oracle, p, chunk, padded):
 @pytest.mark.parametrize("mode,group,n_rs,n_xor", [("0", "1", 1, 1), ("1", "1", 11, 8), ("1", "3", 4, 3),
                                                    ("2", "1", 1, 1), ("3", "2", 6, 4), ("3", "0", 1, 1),
                                                    ("3", "1", 11, 8), ("4", "0", 1, 8), ("4", "3", 4, 3)])
+@pytest.mark.knobs
 def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     """A plan runs its stripes side by side in one launch (REDSET_HIP_SEQUENTIAL=0),
     one launch per stripe (=1, the default for cells >= 24 MiB but RS(8+3)'s; or
@@ -301,6 +302,7 @@ def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
 
 
 @pytest.mark.parametrize("mode", ["2", "0", "1", "3", "4"])
+@pytest.mark.knobs
 def test_ring_jobs_back_to_back(rd, oracle, monkeypatch, mode):
     """The kernels' loader-wave ring is reused job after job inside one launch
     (REDSET_HIP_SEQUENTIAL=2: every block loops over the stripes) and launch
@@ -331,6 +333,86 @@ def test_ring_jobs_back_to_back(rd, oracle, monkeypatch, mode):
         _, xgot = download_set(xlay)
         assert all(np.array_equal(a, b) for a, b in zip(got, parity))
         assert all(np.array_equal(a, b) for a, b in zip(xgot, xc))
+
+
+def _window_set(cells_of, p, ncell, chunk, lo, hi):
+    """[lo, hi) of every cell of every member, cells back to back (what the
+    oracle's set functions take, with chunk_size = hi - lo)"""
+    return [np.concatenate([cells_of(r, s)[lo:hi].cpu().numpy() for s in range(ncell)]) for r in range(p)]
+
+
+@pytest.mark.knobs
+@pytest.mark.parametrize("chunk", [(4 << 20) + 5 * 1024 + 48, (4 << 20) + 7 * 1024])
+def test_claimed_order_ragged_rows(rd, oracle, monkeypatch, chunk):
+    """The claimed order (REDSET_HIP_SEQUENTIAL=4, RS(8+3)'s default encode
+    for cells >= 24 MiB) at a size the fast suite can afford: >= 256 blocks,
+    so the grid is a multiple of 8 and every XCD's queue is used, and a row
+    count (4102 / 4103 rows of 1 KiB, the first with a 48-byte last row) that
+    nq * batch = 32 does not divide, so queues end mid-batch and rows past
+    the end are skipped. Encode and a 3-member rebuild, both
+    claimed, against the oracle."""
+    monkeypatch.setenv("REDSET_HIP_SEQUENTIAL", "4")
+    p, e, lost = 11, 3, [2, 6, 7]
+    lofi, parity = oracle.random_set(p, p - e, e, chunk, seed=chunk % 1000)
+    lay = upload_set(rd, lofi, parity, p - e, e, chunk)
+    codec = rd.RSCodec(p, e)
+    enc = codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    assert enc.launches == 1
+    for _ in range(3):  # repeated launches start from zeroed queues
+        enc.execute()
+    torch.cuda.synchronize()
+    oracle.OracleRS(p, e).encode_set(lofi, parity, chunk)
+    _, got = download_set(lay)
+    assert all(np.array_equal(a, b) for a, b in zip(got, parity))
+    for r in lost:
+        lay.lofi(r).fill_(0x5A)
+        lay.parity(r).fill_(0xA5)
+    reb = codec.plan_rebuild(lost, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    assert reb.launches == 1
+    reb.execute()
+    torch.cuda.synchronize()
+    gl, gp = download_set(lay)
+    assert all(np.array_equal(a, b) for a, b in zip(gl, lofi))
+    assert all(np.array_equal(a, b) for a, b in zip(gp, parity))
+
+
+def test_claimed_encode_product_ragged_rows(rd, oracle):
+    """The product library's own choice at a ragged big size: RS(8+3) with
+    24 MiB + 5 KiB + 48 B cells encodes as ONE claimed launch (8 queues,
+    24582 rows, not a multiple of 32) and rebuilds in streamed pairs. Cells
+    are random on the device; three windows of every cell -- the start, the
+    middle, and the ragged end -- are checked against the oracle, and the
+    whole set by an encode -> erase -> rebuild round trip."""
+    p, e, lost = 11, 3, [1, 4]
+    d = p - e
+    chunk = (24 << 20) + 5 * 1024 + 48
+    lay = rd.SetLayout.allocate(p, d, e, chunk)
+    g = torch.Generator(device="cuda")
+    g.manual_seed(11)
+    lay.storage.copy_(torch.randint(0, 256, lay.storage.shape, dtype=torch.uint8, device="cuda", generator=g))
+    codec = rd.RSCodec(p, e)
+    enc = codec.plan_encode(lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    assert enc.launches == 1  # claimed: the whole set in one launch
+    enc.execute()
+    enc.execute()
+    torch.cuda.synchronize()
+    ref = lay.storage.clone()
+    ora = oracle.OracleRS(p, e)
+    for lo, hi in [(0, 65536), (chunk // 2 - 4096, chunk // 2 + 4096), (chunk - 70_000, chunk)]:
+        wl = _window_set(lay.data_cell, p, d, chunk, lo, hi)
+        wp = [np.zeros(e * (hi - lo), np.uint8) for _ in range(p)]
+        ora.encode_set(wl, wp, hi - lo)
+        got = _window_set(lay.parity_cell, p, e, chunk, lo, hi)
+        assert all(np.array_equal(a, b) for a, b in zip(got, wp)), (lo, hi)
+    for r in lost:  # the cells only: the pad bytes between them are no one's
+        for s in range(d):
+            lay.data_cell(r, s).fill_(0)
+        for i in range(e):
+            lay.parity_cell(r, i).fill_(0)
+    reb = codec.plan_rebuild(lost, lay.lofi_ptrs(), lay.parity_ptrs(), chunk, lay.cell_stride)
+    reb.execute()
+    torch.cuda.synchronize()
+    assert torch.equal(lay.storage, ref)
 
 
 def test_zero_length_calls_are_noops(rd):

@@ -170,12 +170,13 @@ def test_file_round_trip_crc(rd, oracle, tmp_path, scheme):
         assert np.array_equal(got, want[r]), r
 
 
-@pytest.mark.parametrize("zero_copy", ["1", "0"])
+@pytest.mark.parametrize("zero_copy", ["1", pytest.param("0", marks=pytest.mark.knobs)])
 @pytest.mark.parametrize("p,e,chunk", [(11, 3, 200_001), (20, 4, 65536)])
 def test_stream_direct_dma_pinned(rd, oracle, monkeypatch, p, e, chunk, zero_copy):
     """page-locked host cells: by default the kernel reads and writes them
-    over PCIe in place (zero copy); REDSET_HIP_ZERO_COPY=0 runs the staged
-    pipeline with direct DMA of the mapped cells instead. Same bytes."""
+    over PCIe in place (zero copy); with the test twin library,
+    REDSET_HIP_ZERO_COPY=0 runs the staged pipeline with direct DMA of the
+    mapped cells instead. Same bytes."""
     monkeypatch.setenv("REDSET_HIP_ZERO_COPY", zero_copy)
     redset_amd, stream = rd
     d = p - e

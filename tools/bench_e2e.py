@@ -25,7 +25,11 @@ def host_case(p, e, chunk, lost, slice_bytes, threads, mode="zero copy"):
     "direct DMA" (staged pipeline, SDMA straight from/to the page-locked cells)
     or "staged" (read/write callbacks through pinned staging buffers)."""
     pinned = mode != "staged"
-    os.environ["REDSET_HIP_ZERO_COPY"] = "1" if mode == "zero copy" else "0"
+    if mode == "direct DMA":
+        # the staged pipeline over mapped cells is a test-twin knob (the
+        # product takes zero copy whenever every cell is mapped)
+        os.environ["REDSET_HIP_ZERO_COPY"] = "0"
+        os.environ.setdefault("REDSET_HIP_LIBRARY", os.path.join(ROOT, "redset_amd", "lib_test", "libredset_hip.so"))
     import torch
     import redset_amd
     from redset_amd import stream

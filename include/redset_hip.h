@@ -316,6 +316,10 @@ typedef struct {
   unsigned long long return_bytes_recv;
   unsigned long long local_bytes;         /* copied within this process */
   unsigned long long compute_bytes;       /* algorithmic bytes of this process's slice */
+  unsigned long long gather_msg_max;      /* largest / smallest peer message this process sends */
+  unsigned long long gather_msg_min;
+  unsigned long long return_msg_max;
+  unsigned long long return_msg_min;
 } redset_hip_sharded_info;
 
 typedef struct redset_hip_sharded redset_hip_sharded;
@@ -336,6 +340,14 @@ size_t redset_hip_shard_slice_bytes(size_t chunk_size, int world);
 int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
                                const redset_hip_shard_layout* layout, const redset_hip_transport* transport,
                                const redset_hip_compute* compute, redset_hip_sharded** out);
+/* The same for an XOR set (e = 1; kind REDSET_HIP_PLAN_XOR_ENCODE, or
+ * REDSET_HIP_PLAN_XOR_REBUILD of member `root`): the layout's cells are the
+ * p - 1 logical-file segments and the one XOR chunk of every member. The
+ * rebuild gathers every survivor's every cell; it replaces the pipelined
+ * reduce to the lost member (src/redset_xor.c:466-524). */
+int redset_hip_xor_sharded_plan(int ranks, int kind, int root, const redset_hip_shard_layout* layout,
+                                const redset_hip_transport* transport, const redset_hip_compute* compute,
+                                redset_hip_sharded** out);
 /* All three phases, ordered after the work already on `stream`; work
  * enqueued on `stream` afterwards sees the results. With the HIP plans as
  * compute (compute == NULL at plan time) the sets are pipelined: every set's
@@ -354,6 +366,8 @@ void redset_hip_sharded_destroy(redset_hip_sharded* plan);
  * channel: MPI_Bcast, torch.distributed, a file), then every process creates
  * its transport collectively (ncclCommInitRank) on its current device. */
 typedef struct redset_hip_rccl redset_hip_rccl;
+/* 1 if librccl can be loaded in this process (no communication), else 0 */
+int redset_hip_rccl_available(void);
 int redset_hip_rccl_unique_id(unsigned char id_out[128]);
 int redset_hip_rccl_transport_create(const unsigned char id[128], int world, int rank, redset_hip_transport* out,
                                      redset_hip_rccl** handle);

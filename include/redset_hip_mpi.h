@@ -50,6 +50,30 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
 int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
                                int fd_chunk, size_t chunk_size, size_t buf_size);
 
+/* The exchange of the multi-rank rebuild (the two decode backends above).
+ * REDSET_HIP_EXCHANGE_AUTO (the default): when the members of `comm` are on
+ * one node and each owns a distinct GPU (PCI bus id) and librccl loads on
+ * every member, the decode runs as the sharded plan over RCCL / xGMI: every
+ * member reads the cells the decode needs into HBM, the plan gathers column
+ * slices of them onto every member's GPU, runs gf_mac on each slice and
+ * returns the rebuilt slices to the lost members (replacing the decode ring
+ * and gather, src/redset_reedsolomon.c:646-733, and the XOR reduce to the
+ * root, src/redset_xor.c:466-524); otherwise the host-MPI path above. The
+ * choice is made once per communicator (cached on it as an MPI attribute,
+ * with the RCCL communicator, freed with it). _HOST_MPI and _SHARDED_RCCL
+ * force a path; _SHARDED_MPI runs the sharded plan over the MPI transport
+ * with device buffers (members may share a GPU). Process-wide; every member
+ * of a set must pass the same mode (the decode checks and fails otherwise).
+ * The exchange a decode used on this thread: redset_hip_rank_last_exchange. */
+enum {
+  REDSET_HIP_EXCHANGE_AUTO = 0,
+  REDSET_HIP_EXCHANGE_HOST_MPI = 1,
+  REDSET_HIP_EXCHANGE_SHARDED_MPI = 2,
+  REDSET_HIP_EXCHANGE_SHARDED_RCCL = 3
+};
+int redset_hip_rank_set_exchange(int mode);
+int redset_hip_rank_last_exchange(void);
+
 /* The backends above keep a successful call's pinned host buffers, device
  * buffers and stream for the next call (at most 256 MiB pinned, 1 GiB of
  * device memory); REDSET_HIP_SCRATCH_CACHE=0 allocates and frees per call

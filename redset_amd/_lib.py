@@ -59,10 +59,12 @@ EXPORTED_SYMBOLS = (
     "redset_hip_fileio_destroy",
     "redset_hip_shard_slice_bytes",
     "redset_hip_rs_sharded_plan",
+    "redset_hip_xor_sharded_plan",
     "redset_hip_sharded_execute",
     "redset_hip_sharded_execute_phase",
     "redset_hip_sharded_get_info",
     "redset_hip_sharded_destroy",
+    "redset_hip_rccl_available",
     "redset_hip_rccl_unique_id",
     "redset_hip_rccl_transport_create",
     "redset_hip_rccl_transport_destroy",
@@ -166,6 +168,10 @@ class ShardedInfo(ctypes.Structure):
         ("return_bytes_recv", c_ulonglong),
         ("local_bytes", c_ulonglong),
         ("compute_bytes", c_ulonglong),
+        ("gather_msg_max", c_ulonglong),
+        ("gather_msg_min", c_ulonglong),
+        ("return_msg_max", c_ulonglong),
+        ("return_msg_min", c_ulonglong),
     ]
 
     def as_dict(self):
@@ -215,10 +221,13 @@ _SIGNATURES = {
     "redset_hip_rs_sharded_plan": (
         c_int, [c_void_p, c_int, c_int, POINTER(c_int), POINTER(ShardLayout), POINTER(Transport), POINTER(Compute),
                 POINTER(c_void_p)]),
+    "redset_hip_xor_sharded_plan": (
+        c_int, [c_int, c_int, c_int, POINTER(ShardLayout), POINTER(Transport), POINTER(Compute), POINTER(c_void_p)]),
     "redset_hip_sharded_execute": (c_int, [c_void_p, c_void_p]),
     "redset_hip_sharded_execute_phase": (c_int, [c_void_p, c_int, c_void_p]),
     "redset_hip_sharded_get_info": (c_int, [c_void_p, POINTER(ShardedInfo)]),
     "redset_hip_sharded_destroy": (None, [c_void_p]),
+    "redset_hip_rccl_available": (c_int, []),
     "redset_hip_rccl_unique_id": (c_int, [POINTER(c_ubyte)]),
     "redset_hip_rccl_transport_create": (c_int, [POINTER(c_ubyte), c_int, c_int, POINTER(Transport), POINTER(c_void_p)]),
     "redset_hip_rccl_transport_destroy": (None, [c_void_p]),

@@ -453,18 +453,12 @@ out:
 #define TAG_RING 0
 #define TAG_GATHER 1
 
-int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missing, const int* rebuild_ranks,
-                              int need_rebuild, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
-                              size_t chunk_size, size_t buf_size) {
-  int p, r, rp, e;
-  off_t header;
-  if (!rs || !lofi || !rebuild_ranks) return fail("rs_decode_rank: null argument");
-  if (comm_geometry(comm, &p, &r) || redset_hip_rs_shape(rs, &rp, &e)) return REDSET_FAILURE;
-  if (p != rp) return fail("communicator has %d ranks, codec %d", p, rp);
-  if (missing < 1 || missing > e) return fail("cannot rebuild %d members with %d encoding blocks", missing, e);
-  const int hrc = header_size(fd_chunk, chunk_file, &header);
-  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
-  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
+/* the host-MPI exchange of the RS decode (members sharing GPUs, several
+ * nodes, or no RCCL): the reference's message pattern through pinned host
+ * memory */
+static int rs_decode_host(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, int e, int missing,
+                          const int* rebuild_ranks, int need_rebuild, const redset_hip_io* lofi, const char* chunk_file,
+                          int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B) {
 
   unsigned char* D = malloc((size_t) missing * p); /* decode map of stripe r: missing x p */
   unsigned char* coef = malloc((size_t) missing * p);
@@ -715,18 +709,10 @@ out:
 
 /* ---- XOR decode (replaces redset_xor_decode, src/redset_xor.c:441-531) */
 
-int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
-                               int fd_chunk, size_t chunk_size, size_t buf_size) {
-  int p, r;
-  off_t header;
-  if (!lofi || !lofi->read) return fail("xor_decode_rank: null argument");
-  if (comm_geometry(comm, &p, &r)) return REDSET_FAILURE;
-  if (root < 0 || root >= p) return fail("root %d out of range", root);
-  /* a bad fd on one member is agreed on below, not returned early: its
-   * peers would wait for it in the first collective */
-  const int hrc = header_size(fd_chunk, chunk_file, &header);
-  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
-  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
+/* the host-MPI exchange of the XOR decode: every survivor's cell of stripe c
+ * to the root, stripe by stripe */
+static int xor_decode_host(MPI_Comm comm, int p, int r, int root, const redset_hip_io* lofi, const char* chunk_file,
+                           int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B) {
 
   const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
   MPI_Request* req = malloc(sizeof(*req) * (size_t) p);
@@ -820,6 +806,354 @@ out:
   free(ins);
   free(req);
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+/* ---- the multi-rank rebuild over the sharded plan (RCCL / xGMI) ---------- */
+/*
+ * When the members of the set each own a GPU of one node, the decode does
+ * not pass cells between hosts at all: every member reads the cells some
+ * stripe's decode needs into HBM, and the sharded plan (sharded.c) gathers
+ * column slices of them onto every member's GPU over the transport -- RCCL
+ * over xGMI --, runs gf_mac on each GPU's slice of every stripe, and returns
+ * the rebuilt slices to the lost members, which write them after the header
+ * as the host path does. This replaces the decode's ring and its gather to
+ * the failed ranks (src/redset_reedsolomon.c:646-703, :713-733) and the XOR
+ * decode's pipelined reduce to the root (src/redset_xor.c:466-524).
+ *
+ * The chunk goes in windows of at most kWindow bytes of staging per cell set
+ * (double-buffered: the reads of window n+1 overlap the exchange and the
+ * kernels of window n). Each window starts with one MPI_Allreduce(LAND) of
+ * every member's state, so a read or device error on one member stops every
+ * member before the next exchange: all return failure, none hangs (the
+ * reference keeps its ring going instead, :666-681; the caller's AND-reduce
+ * fails the call either way).
+ */
+#define SHARDED_WINDOW ((size_t) 96 << 20) /* host staging per window buffer, all cells */
+
+static int g_exchange_mode = REDSET_HIP_EXCHANGE_AUTO;
+static __thread int g_last_exchange = 0;
+
+int redset_hip_rank_set_exchange(int mode) {
+  if (mode < REDSET_HIP_EXCHANGE_AUTO || mode > REDSET_HIP_EXCHANGE_SHARDED_RCCL)
+    return fail("rank_set_exchange: unknown mode %d", mode);
+  g_exchange_mode = mode;
+  return REDSET_SUCCESS;
+}
+
+int redset_hip_rank_last_exchange(void) { return g_last_exchange; }
+
+/* per-communicator exchange, decided once and cached on the communicator
+ * (an MPI attribute: the RCCL communicator is destroyed with it) */
+typedef struct {
+  int mode;                /* REDSET_HIP_EXCHANGE_HOST_MPI or _SHARDED_RCCL */
+  redset_hip_transport tr;
+  redset_hip_rccl* rccl;
+} comm_exchange;
+
+static int exch_keyval = MPI_KEYVAL_INVALID;
+
+static int exch_delete(MPI_Comm comm, int keyval, void* attr, void* extra) {
+  (void) comm, (void) keyval, (void) extra;
+  comm_exchange* X = (comm_exchange*) attr;
+  if (X) redset_hip_rccl_transport_destroy(X->rccl);
+  free(X);
+  return MPI_SUCCESS;
+}
+
+/* members on one node, each with its own GPU, and librccl loadable on every
+ * member (collective; the same answer on every member) */
+static int rccl_possible(MPI_Comm comm, int p, int r) {
+  int ok = 1;
+  MPI_Comm node;
+  if (MPI_Comm_split_type(comm, MPI_COMM_TYPE_SHARED, r, MPI_INFO_NULL, &node) == MPI_SUCCESS) {
+    int n = 0;
+    MPI_Comm_size(node, &n);
+    ok = n == p;
+    MPI_Comm_free(&node);
+  } else {
+    ok = 0;
+  }
+  char bus[64];
+  memset(bus, 0, sizeof(bus));
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetPCIBusId(bus, (int) sizeof(bus) - 1, dev) != hipSuccess) ok = 0;
+  char* all = malloc((size_t) p * sizeof(bus));
+  if (!all) ok = 0;
+  if (all && MPI_Allgather(bus, (int) sizeof(bus), MPI_CHAR, all, (int) sizeof(bus), MPI_CHAR, comm) == MPI_SUCCESS) {
+    for (int a = 0; a < p && ok; ++a)
+      for (int b = a + 1; b < p && ok; ++b)
+        if (strncmp(all + (size_t) a * sizeof(bus), all + (size_t) b * sizeof(bus), sizeof(bus)) == 0) ok = 0;
+  } else {
+    ok = 0;
+  }
+  free(all);
+  ok = ok && redset_hip_rccl_available();
+  int all_ok = 0;
+  if (MPI_Allreduce(&ok, &all_ok, 1, MPI_INT, MPI_LAND, comm) != MPI_SUCCESS) return 0;
+  return all_ok;
+}
+
+/* a one-rank-per-GPU RCCL communicator over comm's members (collective) */
+static int rccl_create(MPI_Comm comm, int p, int r, comm_exchange* X) {
+  unsigned char id[129];
+  memset(id, 0, sizeof(id));
+  if (r == 0) id[128] = redset_hip_rccl_unique_id(id) == REDSET_SUCCESS;
+  if (MPI_Bcast(id, (int) sizeof(id), MPI_BYTE, 0, comm) != MPI_SUCCESS) return fail("MPI_Bcast failed");
+  if (!id[128]) return fail("RCCL unique id failed on member 0");
+  int rc = redset_hip_rccl_transport_create(id, p, r, &X->tr, &X->rccl);
+  int ok = rc == 0, all = 0;
+  if (MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_LAND, comm) != MPI_SUCCESS) return fail("MPI_Allreduce failed");
+  if (!all) {
+    redset_hip_rccl_transport_destroy(X->rccl);
+    X->rccl = NULL;
+    return rc ? rc : fail("a peer's RCCL communicator failed");
+  }
+  return 0;
+}
+
+/* The exchange of this decode (collective): the process's mode -- every
+ * member must set the same one -- and, for AUTO, RCCL when the members each
+ * own a GPU of one node, else the host path. *tr is set for the sharded
+ * modes; *mpi_t is a transport to destroy after the call (SHARDED_MPI). */
+static int choose_exchange(MPI_Comm comm, int p, int r, int* mode, redset_hip_transport* tr,
+                           redset_hip_mpi_transport** mpi_t) {
+  int m[2] = {g_exchange_mode, -g_exchange_mode}, mm[2];
+  *mpi_t = NULL;
+  if (MPI_Allreduce(m, mm, 2, MPI_INT, MPI_MAX, comm) != MPI_SUCCESS) return fail("MPI_Allreduce failed");
+  if (mm[0] != -mm[1]) return fail("members disagree on the rebuild exchange (redset_hip_rank_set_exchange)");
+  *mode = m[0];
+  if (*mode == REDSET_HIP_EXCHANGE_HOST_MPI) return 0;
+  if (*mode == REDSET_HIP_EXCHANGE_SHARDED_MPI) {
+    /* the sharded plan over MPI with device buffers staged through pinned
+     * memory: members may share a GPU (tests, or nodes without RCCL) */
+    int rc = redset_hip_mpi_transport_create(comm, 1, tr, mpi_t);
+    return agree_setup(comm, rc);
+  }
+  if (exch_keyval == MPI_KEYVAL_INVALID &&
+      MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, exch_delete, &exch_keyval, NULL) != MPI_SUCCESS)
+    return fail("MPI_Comm_create_keyval failed");
+  comm_exchange* X = NULL;
+  int found = 0;
+  if (MPI_Comm_get_attr(comm, exch_keyval, &X, &found) != MPI_SUCCESS) return fail("MPI_Comm_get_attr failed");
+  if (!found) {
+    X = calloc(1, sizeof(*X));
+    if (!X) return fail("out of host memory");
+    X->mode = REDSET_HIP_EXCHANGE_HOST_MPI;
+    if (*mode == REDSET_HIP_EXCHANGE_SHARDED_RCCL || rccl_possible(comm, p, r)) {
+      if (rccl_create(comm, p, r, X) == 0) X->mode = REDSET_HIP_EXCHANGE_SHARDED_RCCL;
+      else if (*mode == REDSET_HIP_EXCHANGE_SHARDED_RCCL) {
+        free(X);
+        return REDSET_FAILURE;
+      }
+    }
+    if (MPI_Comm_set_attr(comm, exch_keyval, X) != MPI_SUCCESS) {
+      exch_delete(comm, exch_keyval, X, NULL);
+      return fail("MPI_Comm_set_attr failed");
+    }
+  }
+  if (*mode == REDSET_HIP_EXCHANGE_SHARDED_RCCL && X->mode != REDSET_HIP_EXCHANGE_SHARDED_RCCL)
+    return fail("RCCL exchange requested, but this communicator uses the host path");
+  *mode = X->mode;
+  *tr = X->tr;
+  return 0;
+}
+
+/* member r's cell in stripe c: data cell x (0 <= x < d) or parity slot
+ * d + i, as sharded.c cell_of numbers them */
+static int member_cell(int p, int e, int xor_scheme, int r, int c) {
+  if (xor_scheme) return c == r ? p - 1 : xor_segment(r, c);
+  const int enc = redset_hip_rs_get_encoding_id(p, e, r, c);
+  return enc < p ? redset_hip_rs_get_data_id(p, e, r, c) : (p - e) + (enc - p);
+}
+
+/* rs == NULL: XOR (e = 1, the root is lost[0]) */
+static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, int e, int missing, const int* lost,
+                          int need_rebuild, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
+                          off_t header, int hrc, size_t chunk_size, size_t B, const redset_hip_transport* tr) {
+  const int d = p - e, ncell = p, world = p;
+  const int xor_scheme = rs == NULL;
+  size_t win = SHARDED_WINDOW / (size_t) ncell;
+  if (win < B) win = B;
+  if (win > chunk_size) win = chunk_size;
+  if (win == 0) win = 1;
+  const size_t W = redset_hip_shard_slice_bytes(win, world);
+  const size_t WW = W * (size_t) world; /* one cell's window in the host image */
+  const size_t nwin = chunk_size ? (chunk_size + win - 1) / win : 0;
+  const size_t tail = chunk_size - (nwin ? (nwin - 1) * win : 0);
+
+  unsigned char* want = calloc((size_t) ncell, 1); /* cells of mine some stripe's decode reads */
+  unsigned char* D = malloc((size_t) missing * p);
+  int* host = malloc(sizeof(int) * (size_t) p);
+  int* slot = calloc((size_t) p, sizeof(int));
+  scratch S;
+  scratch_init(&S);
+  uint8_t* h_img[2] = {scratch_host(&S, (size_t) ncell * WW), scratch_host(&S, (size_t) ncell * WW)};
+  uint8_t* hd[2] = {scratch_dev(&S, (size_t) world * d * W), scratch_dev(&S, (size_t) world * d * W)};
+  uint8_t* hp[2] = {scratch_dev(&S, (size_t) world * e * W), scratch_dev(&S, (size_t) world * e * W)};
+  uint8_t* gd[2] = {scratch_dev(&S, (size_t) world * d * W), scratch_dev(&S, (size_t) world * d * W)};
+  uint8_t* gp[2] = {scratch_dev(&S, (size_t) world * e * W), scratch_dev(&S, (size_t) world * e * W)};
+  redset_hip_sharded* plan[2][2] = {{NULL, NULL}, {NULL, NULL}}; /* [buffer][tail window] */
+  hipEvent_t ev[2] = {NULL, NULL};
+  int rc = S.rc ? S.rc : hrc;
+  for (int k = 0; k < 2 && !rc; ++k)
+    if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
+  if (!rc && (!want || !D || !host || !slot)) rc = fail("out of host memory");
+  if (!rc && need_rebuild && !lofi->write) rc = fail("lofi has no write callback");
+  /* which of my cells the decode reads (the sharded plan sends exactly those) */
+  for (int c = 0; c < p && !rc && !need_rebuild; ++c) {
+    int used = xor_scheme;
+    if (!xor_scheme) {
+      rc = redset_hip_rs_decode_matrix(rs, missing, lost, c, D);
+      for (int i = 0; i < missing && !rc; ++i) used |= D[(size_t) i * p + r] != 0;
+    }
+    if (used) want[member_cell(p, e, xor_scheme, r, c)] = 1;
+  }
+  for (int m = 0; m < p && host; ++m) host[m] = m;
+  if ((rc = agree_setup(comm, rc))) goto out;
+
+  int stopped = 0;
+  for (size_t n = 0; n <= nwin; ++n) {
+    const int b = (int) (n & 1);
+    const size_t off = n * win, len = n + 1 == nwin ? tail : win;
+    if (n < nwin) {
+      /* buffers b were last used by window n - 2, written at window n - 1 */
+      if (n >= 2 && !rc && hipEventSynchronize(ev[b]) != hipSuccess) rc = fail("device work failed");
+      /* the plan of buffers b for a whole window, or for the tail window
+       * (planning is local: no communication, every member the same) */
+      redset_hip_sharded** P = &plan[b][len != win];
+      if (!rc && !*P) {
+        redset_hip_shard_layout L = {1, host, slot, 1, len, W, hd[b], hp[b], gd[b], gp[b]};
+        rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, tr, NULL, P)
+                        : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, tr, NULL, P);
+      }
+      uint8_t* img = h_img[b];
+      for (int x = 0; x < ncell && !rc; ++x) {
+        if (!want[x]) continue;
+        uint8_t* dst = img + (size_t) x * WW;
+        if (x < d) {
+          if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, x, off, len, dst) != 0) rc = fail("lofi read failed");
+        } else if (pread_full(fd_chunk, dst, len, header + (off_t) (x - d) * (off_t) chunk_size + (off_t) off) != 0) {
+          rc = fail("read %s failed", chunk_file);
+        }
+      }
+      /* every member's state before the exchange: one failure stops all */
+      int ok = rc == 0, all = 0;
+      if (MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_LAND, comm) != MPI_SUCCESS) rc = fail("MPI_Allreduce failed");
+      if (!all) {
+        if (!rc) rc = fail("a peer's read or device step failed");
+        stopped = 1;
+        break;
+      }
+      hipStream_t s = S.stream;
+      for (int x = 0; x < ncell && !rc; ++x) {
+        if (!want[x]) continue;
+        uint8_t* dst = x < d ? hd[b] + (size_t) x * W : hp[b] + (size_t) (x - d) * W;
+        const size_t dpitch = (size_t) (x < d ? d : e) * W;
+        if (hipMemcpy2DAsync(dst, dpitch, img + (size_t) x * WW, W, W, (size_t) world, hipMemcpyHostToDevice, s) !=
+            hipSuccess)
+          rc = fail("H2D copy failed");
+      }
+      if (!rc && redset_hip_sharded_execute(*P, s) != 0) rc = REDSET_FAILURE;
+      for (int x = 0; x < ncell && !rc && need_rebuild; ++x) {
+        const uint8_t* src = x < d ? hd[b] + (size_t) x * W : hp[b] + (size_t) (x - d) * W;
+        const size_t spitch = (size_t) (x < d ? d : e) * W;
+        if (hipMemcpy2DAsync(img + (size_t) x * WW, W, src, spitch, W, (size_t) world, hipMemcpyDeviceToHost, s) !=
+            hipSuccess)
+          rc = fail("D2H copy failed");
+      }
+      if (!rc && hipEventRecord(ev[b], s) != hipSuccess) rc = fail("hipEventRecord failed");
+    }
+    /* window n - 1's rebuilt cells, after the header as the host path writes them */
+    if (n >= 1 && need_rebuild && !rc) {
+      const int pb = 1 - b;
+      const size_t poff = (n - 1) * win, plen = n == nwin ? tail : win;
+      if (hipEventSynchronize(ev[pb]) != hipSuccess) rc = fail("device work failed");
+      for (int x = 0; x < ncell && !rc; ++x) {
+        const uint8_t* cell = h_img[pb] + (size_t) x * WW;
+        if (x < d) {
+          if (lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, x, poff, plen, cell) != 0) rc = fail("lofi write failed");
+        } else if (pwrite_full(fd_chunk, cell, plen, header + (off_t) (x - d) * (off_t) chunk_size + (off_t) poff) != 0) {
+          rc = fail("write %s failed", chunk_file);
+        }
+      }
+    }
+  }
+  (void) stopped;
+out:
+  if (S.stream) (void) hipStreamSynchronize(S.stream);
+  for (int b = 0; b < 2; ++b)
+    for (int t = 0; t < 2; ++t) redset_hip_sharded_destroy(plan[b][t]);
+  scratch_free(&S, rc == 0);
+  for (int k = 0; k < 2; ++k)
+    if (ev[k]) (void) hipEventDestroy(ev[k]);
+  free(want);
+  free(D);
+  free(host);
+  free(slot);
+  return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missing, const int* rebuild_ranks,
+                              int need_rebuild, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
+                              size_t chunk_size, size_t buf_size) {
+  int p, r, rp, e;
+  off_t header;
+  if (!rs || !lofi || !rebuild_ranks) return fail("rs_decode_rank: null argument");
+  if (comm_geometry(comm, &p, &r) || redset_hip_rs_shape(rs, &rp, &e)) return REDSET_FAILURE;
+  if (p != rp) return fail("communicator has %d ranks, codec %d", p, rp);
+  if (missing < 1 || missing > e) return fail("cannot rebuild %d members with %d encoding blocks", missing, e);
+  for (int i = 0; i < missing; ++i)
+    if (rebuild_ranks[i] < 0 || rebuild_ranks[i] >= p || (i && rebuild_ranks[i] <= rebuild_ranks[i - 1]))
+      return fail("rebuild ranks must be ascending members of 0..%d", p - 1); /* same on every rank */
+  /* a bad fd on one member is agreed on later, not returned early: its
+   * peers would wait for it in the first collective */
+  const int hrc = header_size(fd_chunk, chunk_file, &header);
+  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
+  int mode;
+  redset_hip_transport tr;
+  redset_hip_mpi_transport* mt = NULL;
+  if (choose_exchange(comm, p, r, &mode, &tr, &mt)) {
+    redset_hip_mpi_transport_destroy(mt);
+    return REDSET_FAILURE;
+  }
+  g_last_exchange = mode;
+  int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
+               ? rs_decode_host(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
+                                header, hrc, chunk_size, B)
+               : decode_sharded(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
+                                header, hrc, chunk_size, B, &tr);
+  redset_hip_mpi_transport_destroy(mt);
+  return rc;
+}
+
+int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
+                               int fd_chunk, size_t chunk_size, size_t buf_size) {
+  int p, r;
+  off_t header;
+  if (!lofi || !lofi->read) return fail("xor_decode_rank: null argument");
+  if (comm_geometry(comm, &p, &r)) return REDSET_FAILURE;
+  if (p < 2) return fail("XOR needs at least 2 ranks");
+  if (root < 0 || root >= p) return fail("root %d out of range", root);
+  /* a bad fd on one member is agreed on later, not returned early: its
+   * peers would wait for it in the first collective */
+  const int hrc = header_size(fd_chunk, chunk_file, &header);
+  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
+  int mode;
+  redset_hip_transport tr;
+  redset_hip_mpi_transport* mt = NULL;
+  if (choose_exchange(comm, p, r, &mode, &tr, &mt)) {
+    redset_hip_mpi_transport_destroy(mt);
+    return REDSET_FAILURE;
+  }
+  g_last_exchange = mode;
+  int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
+               ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B)
+               : decode_sharded(NULL, comm, p, r, 1, 1, &root, r == root, lofi, chunk_file, fd_chunk, header, hrc,
+                                chunk_size, B, &tr);
+  redset_hip_mpi_transport_destroy(mt);
+  return rc;
 }
 
 /* ---- MPI transport of the sharded path (include/redset_hip_mpi.h) ------- */

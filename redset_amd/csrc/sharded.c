@@ -12,7 +12,10 @@
  * return; for encode, the ring of redset_reedsolomon_encode (:329-377).
  * Stripe ownership differs on purpose: the reference has rank r solve stripe
  * r whole (:606-611); here every GPU solves its column slice of every stripe,
- * so the work splits evenly whatever p and the number of GPUs.
+ * so the work splits evenly whatever p and the number of GPUs. XOR sets
+ * (redset_hip_xor_sharded_plan) work the same way: the rebuild replaces the
+ * pipelined reduce to the lost member (src/redset_xor.c:466-524), whose root
+ * receives every survivor's every cell, with slices gathered onto every GPU.
  */
 #include <hip/hip_runtime_api.h>
 #include <stdarg.h>
@@ -117,23 +120,31 @@ static int ex_copy(exch* X, unsigned char* dst, const unsigned char* src, size_t
   return rc ? rc : xl_push(L, b);
 }
 
+/* message statistics of one phase (the info block) */
+typedef struct {
+  int* messages;
+  unsigned long long *sent, *recvd, *local, *max_msg, *min_msg;
+} xstats;
+
 /* flatten into one list for the transport: local copies, then per peer its
- * sends and receives; byte counts for the info block */
-static int ex_flatten(exch* X, xlist* out, int* messages, unsigned long long* sent, unsigned long long* recvd,
-                      unsigned long long* local) {
+ * sends and receives; byte counts and message sizes for the info block */
+static int ex_flatten(exch* X, xlist* out, const xstats* st) {
   for (int i = 0; i < X->copy.n; ++i) {
     if (xl_push(out, X->copy.v[i])) return REDSET_FAILURE;
-    if (X->copy.v[i].send) *local += X->copy.v[i].len;
+    if (X->copy.v[i].send) *st->local += X->copy.v[i].len;
   }
   for (int g = 0; g < X->world; ++g) {
     for (int i = 0; i < X->send[g].n; ++i) {
+      const unsigned long long len = X->send[g].v[i].len;
       if (xl_push(out, X->send[g].v[i])) return REDSET_FAILURE;
-      *sent += X->send[g].v[i].len;
-      ++*messages;
+      *st->sent += len;
+      ++*st->messages;
+      if (len > *st->max_msg) *st->max_msg = len;
+      if (*st->min_msg == 0 || len < *st->min_msg) *st->min_msg = len;
     }
     for (int i = 0; i < X->recv[g].n; ++i) {
       if (xl_push(out, X->recv[g].v[i])) return REDSET_FAILURE;
-      *recvd += X->recv[g].v[i].len;
+      *st->recvd += X->recv[g].v[i].len;
     }
   }
   return 0;
@@ -169,15 +180,29 @@ size_t redset_hip_shard_slice_bytes(size_t chunk_size, int world) {
   return (w + 255) & ~(size_t) 255;
 }
 
+static int is_encode(int kind) { return kind == REDSET_HIP_PLAN_RS_ENCODE || kind == REDSET_HIP_PLAN_XOR_ENCODE; }
+static int is_xor(int kind) { return kind == REDSET_HIP_PLAN_XOR_ENCODE || kind == REDSET_HIP_PLAN_XOR_REBUILD; }
+
 /* Which cells of each member some stripe's decode reads: need[r*p + c] for
  * member r's cell in stripe c (data or parity, whichever it is). Encode
- * reads every data cell. */
+ * reads every data cell; an XOR rebuild every cell of every survivor
+ * (src/redset_xor_serial.c:202-273). */
 static int plan_inputs(const redset_hip_rs* rs, int p, int e, int kind, int missing, const int* lost,
                        unsigned char* need) {
   memset(need, 0, (size_t) p * p);
   if (kind == REDSET_HIP_PLAN_RS_ENCODE) {
     for (int r = 0; r < p; ++r)
       for (int c = 0; c < p; ++c) need[r * p + c] = redset_hip_rs_get_encoding_id(p, e, r, c) < p;
+    return 0;
+  }
+  if (kind == REDSET_HIP_PLAN_XOR_ENCODE) {
+    for (int r = 0; r < p; ++r)
+      for (int c = 0; c < p; ++c) need[r * p + c] = c != r; /* member r's parity is stripe r */
+    return 0;
+  }
+  if (kind == REDSET_HIP_PLAN_XOR_REBUILD) {
+    for (int r = 0; r < p; ++r)
+      for (int c = 0; c < p; ++c) need[r * p + c] = r != lost[0];
     return 0;
   }
   unsigned char* D = malloc((size_t) missing * p);
@@ -195,8 +220,11 @@ static int plan_inputs(const redset_hip_rs* rs, int p, int e, int kind, int miss
   return 0;
 }
 
-/* member r's cell in stripe c: data cell index, or -(1 + parity slot) */
-static int cell_of(int p, int e, int r, int c) {
+/* member r's cell in stripe c: data cell index, or -(1 + parity slot).
+ * XOR: stripe r is member r's parity, stripe c != r its logical-file
+ * segment c or c - 1 (src/redset_xor.c:251-266). */
+static int cell_of(int p, int e, int kind, int r, int c) {
+  if (is_xor(kind)) return c == r ? -1 : (c < r ? c : c - 1);
   const int enc = redset_hip_rs_get_encoding_id(p, e, r, c);
   return enc < p ? redset_hip_rs_get_data_id(p, e, r, c) : -(1 + (enc - p));
 }
@@ -228,7 +256,7 @@ static unsigned char* gp(const pctx* C, int h, int j, int i) {
 /* does some stripe read member r's data cell x (pass 0) / parity slot x (pass 1)? */
 static int wanted(const pctx* C, int r, int pass, int x) {
   for (int c = 0; c < C->p; ++c)
-    if (C->need[r * C->p + c] && cell_of(C->p, C->e, r, c) == (pass == 0 ? x : -(1 + x))) return 1;
+    if (C->need[r * C->p + c] && cell_of(C->p, C->e, C->kind, r, c) == (pass == 0 ? x : -(1 + x))) return 1;
   return 0;
 }
 
@@ -269,9 +297,9 @@ static int plan_gather(const pctx* C, int k, exch* G) {
 static int plan_return(const pctx* C, int k, exch* R) {
   int rc = 0;
   for (int pass = 0; pass < 2 && !rc; ++pass) {
-    if (pass == 0 && C->kind == REDSET_HIP_PLAN_RS_ENCODE) continue; /* encode returns parity only */
+    if (pass == 0 && is_encode(C->kind)) continue; /* encode returns parity only */
     for (int m = k * C->p; m < (k + 1) * C->p && !rc; ++m) {
-      int is_out = C->kind == REDSET_HIP_PLAN_RS_ENCODE;
+      int is_out = is_encode(C->kind);
       for (int i = 0; i < C->missing; ++i) is_out |= C->lost[i] == m % C->p;
       if (!is_out) continue;
       const int h = C->L->host[m], j = C->L->slot[m];
@@ -290,18 +318,12 @@ static int plan_return(const pctx* C, int k, exch* R) {
   return rc;
 }
 
-int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
-                               const redset_hip_shard_layout* L, const redset_hip_transport* tr,
-                               const redset_hip_compute* comp, redset_hip_sharded** out) {
-  int p, e;
-  if (!out) return sfail("sharded_plan: null out-pointer");
-  *out = NULL;
-  if (!rs || !L || !tr || !tr->exchange) return sfail("sharded_plan: null argument");
-  if (redset_hip_rs_shape(rs, &p, &e)) return REDSET_FAILURE;
-  if (kind != REDSET_HIP_PLAN_RS_ENCODE && kind != REDSET_HIP_PLAN_RS_REBUILD)
-    return sfail("sharded_plan: kind %d is not RS encode or rebuild", kind);
-  if (kind == REDSET_HIP_PLAN_RS_ENCODE) missing = 0;
-  if (kind == REDSET_HIP_PLAN_RS_REBUILD) {
+/* the plan of either scheme: rs (RS kinds) or NULL (XOR kinds, e = 1) */
+static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missing, const int* rebuild_ranks,
+                     const redset_hip_shard_layout* L, const redset_hip_transport* tr, const redset_hip_compute* comp,
+                     redset_hip_sharded** out) {
+  if (is_encode(kind)) missing = 0;
+  if (!is_encode(kind)) {
     if (missing < 1 || missing > e) return sfail("cannot rebuild %d members with %d parity chunks", missing, e);
     if (!rebuild_ranks) return sfail("null rebuild_ranks");
     for (int i = 0; i < missing; ++i)
@@ -372,11 +394,13 @@ int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, c
   /* set by set, so a set's exchanges can run on their own (pipelined execute) */
   for (int k = 0; k < L->nsets && !rc; ++k) {
     rc = plan_gather(&C, k, &G);
-    if (!rc) rc = ex_flatten(&G, &P->gather, &P->info.gather_messages, &P->info.gather_bytes_sent,
-                             &P->info.gather_bytes_recv, &P->info.local_bytes);
+    const xstats gs = {&P->info.gather_messages, &P->info.gather_bytes_sent, &P->info.gather_bytes_recv,
+                       &P->info.local_bytes, &P->info.gather_msg_max, &P->info.gather_msg_min};
+    const xstats rs_ = {&P->info.return_messages, &P->info.return_bytes_sent, &P->info.return_bytes_recv,
+                        &P->info.local_bytes, &P->info.return_msg_max, &P->info.return_msg_min};
+    if (!rc) rc = ex_flatten(&G, &P->gather, &gs);
     if (!rc) rc = plan_return(&C, k, &R);
-    if (!rc) rc = ex_flatten(&R, &P->ret, &P->info.return_messages, &P->info.return_bytes_sent,
-                             &P->info.return_bytes_recv, &P->info.local_bytes);
+    if (!rc) rc = ex_flatten(&R, &P->ret, &rs_);
     P->goff[k + 1] = P->gather.n;
     P->roff[k + 1] = P->ret.n;
     ex_free(&G);
@@ -399,12 +423,18 @@ int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, c
     P->parity[m] = gp(&C, L->host[m], L->slot[m], 0);
   }
   const size_t n = P->info.my_slice_len;
-  P->info.compute_bytes = (unsigned long long) L->nsets * p * (d + (kind == REDSET_HIP_PLAN_RS_ENCODE ? e : missing)) * n;
+  P->info.compute_bytes = (unsigned long long) L->nsets * p * (d + (is_encode(kind) ? e : missing)) * n;
   for (int k = 0; k < L->nsets && !rc && n > 0 && !P->comp.run; ++k) {
     unsigned char* const* lf = P->lofi + (size_t) k * p;
     unsigned char* const* pr = P->parity + (size_t) k * p;
-    rc = kind == REDSET_HIP_PLAN_RS_ENCODE ? redset_hip_rs_plan_encode(rs, lf, pr, n, W, &P->plans[k])
-                                           : redset_hip_rs_plan_rebuild(rs, missing, P->lost, lf, pr, n, W, &P->plans[k]);
+    switch (kind) {
+      case REDSET_HIP_PLAN_RS_ENCODE: rc = redset_hip_rs_plan_encode(rs, lf, pr, n, W, &P->plans[k]); break;
+      case REDSET_HIP_PLAN_RS_REBUILD:
+        rc = redset_hip_rs_plan_rebuild(rs, missing, P->lost, lf, pr, n, W, &P->plans[k]);
+        break;
+      case REDSET_HIP_PLAN_XOR_ENCODE: rc = redset_hip_xor_plan_encode(p, lf, pr, n, W, &P->plans[k]); break;
+      default: rc = redset_hip_xor_plan_rebuild(p, P->lost[0], lf, pr, n, W, &P->plans[k]); break;
+    }
   }
 done:
   ex_free(&G);
@@ -417,6 +447,33 @@ done:
   }
   *out = P;
   return REDSET_SUCCESS;
+}
+
+int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
+                               const redset_hip_shard_layout* L, const redset_hip_transport* tr,
+                               const redset_hip_compute* comp, redset_hip_sharded** out) {
+  int p, e;
+  if (!out) return sfail("sharded_plan: null out-pointer");
+  *out = NULL;
+  if (!rs || !L || !tr || !tr->exchange) return sfail("sharded_plan: null argument");
+  if (redset_hip_rs_shape(rs, &p, &e)) return REDSET_FAILURE;
+  if (kind != REDSET_HIP_PLAN_RS_ENCODE && kind != REDSET_HIP_PLAN_RS_REBUILD)
+    return sfail("sharded_plan: kind %d is not RS encode or rebuild", kind);
+  return plan_sets(rs, p, e, kind, missing, rebuild_ranks, L, tr, comp, out);
+}
+
+int redset_hip_xor_sharded_plan(int ranks, int kind, int root, const redset_hip_shard_layout* L,
+                                const redset_hip_transport* tr, const redset_hip_compute* comp,
+                                redset_hip_sharded** out) {
+  if (!out) return sfail("xor_sharded_plan: null out-pointer");
+  *out = NULL;
+  if (!L || !tr || !tr->exchange) return sfail("xor_sharded_plan: null argument");
+  if (ranks < 2 || ranks > MAX_RANKS) return sfail("XOR needs 2..%d ranks, got %d", MAX_RANKS, ranks);
+  if (kind != REDSET_HIP_PLAN_XOR_ENCODE && kind != REDSET_HIP_PLAN_XOR_REBUILD)
+    return sfail("xor_sharded_plan: kind %d is not XOR encode or rebuild", kind);
+  if (kind == REDSET_HIP_PLAN_XOR_REBUILD && (root < 0 || root >= ranks))
+    return sfail("root %d out of range", root);
+  return plan_sets(NULL, ranks, 1, kind, kind == REDSET_HIP_PLAN_XOR_REBUILD ? 1 : 0, &root, L, tr, comp, out);
 }
 
 static int compute_set(redset_hip_sharded* P, int k, void* stream) {

@@ -108,6 +108,11 @@ static int rccl_exchange(void* ctx, const redset_hip_xfer* x, int n, void* strea
   return r == ncclSuccess ? 0 : rfail("ncclGroupEnd", r);
 }
 
+int redset_hip_rccl_available(void) {
+  pthread_once(&rccl_once, rccl_open);
+  return rccl.ok;
+}
+
 int redset_hip_rccl_unique_id(unsigned char id_out[128]) {
   ncclUniqueId id;
   if (!id_out) return redset_hip_record_error("rccl_unique_id: null argument");

@@ -34,6 +34,7 @@
 #include <unistd.h>
 
 #include "redset_hip_backend.h"
+#include "redset_hip_mpi.h" /* the exchange selection, test-side only */
 
 int redset_mpi_buf_size = 1024 * 1024;
 
@@ -101,6 +102,20 @@ static int slot_call(int rs, int encode, const redset_base* d, int missing, int*
                   : redset_reedsolomon_decode_hip(d, missing, lost, need_rebuild, rsf, red, fd, chunk);
   return encode ? redset_xor_encode_hip(d, rsf, red, fd, chunk)
                 : redset_xor_decode_hip(d, missing ? lost[0] : 0, rsf, red, fd, chunk);
+}
+
+static int exchange_mode(const char* s) {
+  return strcmp(s, "host") == 0 ? REDSET_HIP_EXCHANGE_HOST_MPI
+         : strcmp(s, "sharded-mpi") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_MPI
+         : strcmp(s, "rccl") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_RCCL
+                                  : REDSET_HIP_EXCHANGE_AUTO;
+}
+
+static const char* exchange_name(int m) {
+  return m == REDSET_HIP_EXCHANGE_HOST_MPI ? "host"
+         : m == REDSET_HIP_EXCHANGE_SHARDED_MPI ? "sharded-mpi"
+         : m == REDSET_HIP_EXCHANGE_SHARDED_RCCL ? "rccl"
+                                                 : "none";
 }
 
 int main(int argc, char** argv) {
@@ -175,6 +190,11 @@ int main(int argc, char** argv) {
     if (fd < 0 || lseek(fd, (off_t) header, SEEK_SET) < 0) MPI_Abort(MPI_COMM_WORLD, 5);
   }
 
+  /* ADAPTER_TEST_EXCHANGE=host|sharded-mpi|rccl: the rebuild's exchange
+   * (include/redset_hip_mpi.h; default auto, which takes the host path when
+   * the members share the box's one GPU) */
+  const char* ex = getenv("ADAPTER_TEST_EXCHANGE");
+  if (ex && redset_hip_rank_set_exchange(exchange_mode(ex)) != REDSET_SUCCESS) MPI_Abort(MPI_COMM_WORLD, 6);
   const char* rep = getenv("ADAPTER_TEST_REPEAT");
   const int repeat = rep && atoi(rep) > 1 ? atoi(rep) : 1;
   int rc = REDSET_SUCCESS;
@@ -196,6 +216,7 @@ int main(int argc, char** argv) {
   redset_hip_backend_finalize();
   if (rank == 0) printf("adapter_test: %s %s %d ranks chunk %llu x%d: %s\n", argv[1], argv[2], ranks, chunk, repeat,
                         rc == REDSET_SUCCESS ? "ok" : "FAILED");
+  if (rank == 0 && !encode) printf("adapter_test: rebuild exchange %s\n", exchange_name(redset_hip_rank_last_exchange()));
   free(names);
   free(sizes);
   free(fds);

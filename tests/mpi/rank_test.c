@@ -9,6 +9,8 @@
  * Rank r reads <dir>/manifest_<r>.txt:
  *   nfiles \n path size \n ... chunk_size \n header_size \n redundancy_path
  * (written by tests/test_gpu_mpi.py). Exit 0 iff every rank succeeded.
+ * RANK_TEST_EXCHANGE=host|sharded-mpi|rccl: the rebuild's exchange
+ * (redset_hip_rank_set_exchange; default auto). Rank 0 prints the one used.
  * RANK_TEST_FAIL_READ=<rank>: that rank's logical-file reads fail from the
  * second call on (an I/O error in the middle of the collective loop).
  * The HIP runtime is initialised before the timed call (an application that
@@ -48,6 +50,20 @@ static int backend_call(int rs_scheme, int encode, int ranks, int encoding, int 
                 : redset_hip_rs_decode_rank(rs, MPI_COMM_WORLD, missing, lost, need_rebuild, io, red, fd, chunk, buf);
   redset_hip_rs_destroy(rs);
   return rc;
+}
+
+static int exchange_mode(const char* s) {
+  return strcmp(s, "host") == 0 ? REDSET_HIP_EXCHANGE_HOST_MPI
+         : strcmp(s, "sharded-mpi") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_MPI
+         : strcmp(s, "rccl") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_RCCL
+                                  : REDSET_HIP_EXCHANGE_AUTO;
+}
+
+static const char* exchange_name(int m) {
+  return m == REDSET_HIP_EXCHANGE_HOST_MPI ? "host"
+         : m == REDSET_HIP_EXCHANGE_SHARDED_MPI ? "sharded-mpi"
+         : m == REDSET_HIP_EXCHANGE_SHARDED_RCCL ? "rccl"
+                                                 : "none";
 }
 
 int main(int argc, char** argv) {
@@ -119,6 +135,8 @@ int main(int argc, char** argv) {
     if (fd < 0 || lseek(fd, (off_t) header, SEEK_SET) < 0) MPI_Abort(MPI_COMM_WORLD, 5);
   }
 
+  const char* ex = getenv("RANK_TEST_EXCHANGE");
+  if (ex && redset_hip_rank_set_exchange(exchange_mode(ex)) != REDSET_SUCCESS) MPI_Abort(MPI_COMM_WORLD, 6);
   (void) hipFree(NULL); /* runtime init outside the timed region */
   MPI_Barrier(MPI_COMM_WORLD);
   const double t0 = MPI_Wtime();
@@ -129,6 +147,7 @@ int main(int argc, char** argv) {
   double dt = MPI_Wtime() - t0, dmax = 0;
   MPI_Reduce(&dt, &dmax, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
   if (rank == 0) printf("rank_test: %s %s %d ranks chunk %llu buf %zu: %.4f s\n", argv[1], argv[2], ranks, chunk, buf, dmax);
+  if (rank == 0 && !encode) printf("rank_test: rebuild exchange %s\n", exchange_name(redset_hip_rank_last_exchange()));
 
   const char* rep = getenv("RANK_TEST_REPEAT");
   const int repeat = rep && atoi(rep) > 1 ? atoi(rep) : 1;

@@ -8,6 +8,8 @@
  * encode / rebuild without a GPU.
  *
  * usage: sharded_test [--gpu | --gpu-host | --gpu-host-null] <p> <e> <chunk> [lost ranks...]   (world = MPI size)
+ * SHARDED_TEST_SCHEME=xor: an XOR set (redset_hip_xor_sharded_plan; e must be
+ * 1 and the one lost rank is the root), checked against the oracle's XOR.
  * SHARDED_TEST_REPS=<n> (--gpu): after the checks, time n rebuilds with the
  * pipelined execute and n with the three phases one after another (slowest
  * process, ms per rebuild).
@@ -38,7 +40,7 @@
 #include "redset_hip_mpi.h"
 #include "redset_oracle.h"
 
-static int P, E, D;
+static int P, E, D, XOR;
 static ro_rs* ORACLE;
 
 static uint8_t byte_of(int k, int r, size_t i) { /* member (k, r)'s logical-file byte i */
@@ -78,7 +80,10 @@ static int oracle_run(void* ctx, int kind, int missing, const int* lost, unsigne
   }
   int rc = 0;
   if (kind == REDSET_HIP_PLAN_RS_ENCODE) ro_rs_encode_set(ORACLE, n, lf, pr, 1 << 20);
-  else rc = ro_rs_rebuild_set(ORACLE, n, missing, lost, lf, pr, 1 << 20);
+  else if (kind == REDSET_HIP_PLAN_RS_REBUILD) rc = ro_rs_rebuild_set(ORACLE, n, missing, lost, lf, pr, 1 << 20);
+  else if (kind == REDSET_HIP_PLAN_XOR_ENCODE) ro_xor_encode_set(P, n, lf, pr, 1 << 20);
+  else if (missing == 1) ro_xor_rebuild_set(P, n, lost[0], lf, pr, 1 << 20);
+  else rc = 1;
   for (int r = 0; r < P; ++r) {
     for (int s = 0; s < D; ++s) memcpy(lofi[r] + (size_t) s * W, lf[r] + (size_t) s * n, n);
     for (int i = 0; i < E; ++i) memcpy(parity[r] + (size_t) i * W, pr[r] + (size_t) i * n, n);
@@ -107,6 +112,8 @@ int main(int argc, char** argv) {
   P = atoi(argv[1]);
   E = atoi(argv[2]);
   D = P - E;
+  XOR = getenv("SHARDED_TEST_SCHEME") && strcmp(getenv("SHARDED_TEST_SCHEME"), "xor") == 0;
+  if (XOR && E != 1) MPI_Abort(MPI_COMM_WORLD, 2);
   const size_t C = (size_t) atoll(argv[3]);
   const int missing = argc - 4;
   int lost[64];
@@ -147,7 +154,10 @@ int main(int argc, char** argv) {
     want_p[m] = calloc((size_t) E * C, 1);
     for (size_t i = 0; i < (size_t) D * C; ++i) want_l[m][i] = byte_of(m / P, m % P, i);
   }
-  for (int k = 0; k < nsets; ++k) ro_rs_encode_set(ORACLE, C, want_l + k * P, want_p + k * P, 1 << 20);
+  for (int k = 0; k < nsets; ++k) {
+    if (XOR) ro_xor_encode_set(P, C, want_l + k * P, want_p + k * P, 1 << 20);
+    else ro_rs_encode_set(ORACLE, C, want_l + k * P, want_p + k * P, 1 << 20);
+  }
 
   redset_hip_rs* rs = NULL;
   redset_hip_transport tr;
@@ -186,10 +196,16 @@ int main(int argc, char** argv) {
   }
   redset_hip_sharded *enc = NULL, *reb = NULL;
   const redset_hip_compute* cp = gpu ? NULL : &comp;
-  int ok = redset_hip_rs_create(P, E, &rs) == 0 && redset_hip_mpi_transport_create(MPI_COMM_WORLD, host_slabs ? 2 : gpu ? 1 : 0, &tr, &th) == 0 &&
-           redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, &tr, cp, &enc) == 0 &&
-           (missing == 0 ||
-            redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, &tr, cp, &reb) == 0);
+  int ok = (XOR || redset_hip_rs_create(P, E, &rs) == 0) &&
+           redset_hip_mpi_transport_create(MPI_COMM_WORLD, host_slabs ? 2 : gpu ? 1 : 0, &tr, &th) == 0;
+  if (ok && XOR)
+    ok = redset_hip_xor_sharded_plan(P, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, &tr, cp, &enc) == 0 &&
+         (missing == 0 ||
+          (missing == 1 && redset_hip_xor_sharded_plan(P, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, &tr, cp, &reb) == 0));
+  else if (ok)
+    ok = redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, &tr, cp, &enc) == 0 &&
+         (missing == 0 ||
+          redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, &tr, cp, &reb) == 0);
   if (!ok) fprintf(stderr, "rank %d: setup: %s\n", me, redset_hip_last_error());
   int bad = 0;
   if (ok && redset_hip_sharded_execute(enc, stream) != 0) {
@@ -258,8 +274,10 @@ int main(int argc, char** argv) {
     }
     redset_hip_sharded_info info;
     if (ok && redset_hip_sharded_get_info(reb, &info) == 0)
-      printf("rank %d: rebuild gather %llu B sent in %d messages, return %llu B sent, local %llu B\n", me,
-             info.gather_bytes_sent, info.gather_messages, info.return_bytes_sent, info.local_bytes);
+      printf("rank %d: rebuild gather %llu B sent in %d messages (%llu..%llu B), return %llu B sent in %d messages, "
+             "local %llu B\n",
+             me, info.gather_bytes_sent, info.gather_messages, info.gather_msg_min, info.gather_msg_max,
+             info.return_bytes_sent, info.return_messages, info.local_bytes);
   }
   int mine = ok && !bad, all = 0;
   MPI_Allreduce(&mine, &all, 1, MPI_INT, MPI_LAND, MPI_COMM_WORLD);

@@ -39,6 +39,7 @@ def _need():
     assert os.path.exists(DRIVER), f"{DRIVER} missing: build it with `make -C tests/adapter` (needs the reference headers)"
 
 
+@pytest.mark.parametrize("exchange", ["auto", "sharded-mpi"])
 @pytest.mark.parametrize("scheme,p,e,lost,buf,repeat", [
     ("rs", 4, 2, [1, 2], 65536, 1),
     ("rs", 4, 2, [0, 3], 1 << 20, 2),   # the second call reuses the adapter's cached codec
@@ -46,7 +47,14 @@ def _need():
     ("xor", 4, 1, [2], 50000, 1),
     ("xor", 5, 1, [0], 1 << 20, 2),
 ])
-def test_adapter_slot_encode_and_rebuild(oracle, tmp_path, scheme, p, e, lost, buf, repeat):
+def test_adapter_slot_encode_and_rebuild(oracle, tmp_path, scheme, p, e, lost, buf, repeat, exchange):
+    """Encode, lose members, rebuild through the reference-signature slot.
+    exchange "auto": on the box's one GPU the members share a device, so the
+    rebuild takes the host-MPI path; "sharded-mpi": the path redset_recover()
+    takes when every member owns a GPU -- the sharded plan (column slices
+    gathered onto every GPU, gf_mac, rebuilt slices returned) -- over the
+    MPI transport with device buffers in place of RCCL (RCCL needs one GPU
+    per rank)."""
     _need()
     tmp = str(tmp_path)
     d = p - e
@@ -56,7 +64,7 @@ def test_adapter_slot_encode_and_rebuild(oracle, tmp_path, scheme, p, e, lost, b
     reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
     _manifests(tmp, files, chunk, header, reds)
     crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
-    env = {"ADAPTER_TEST_REPEAT": str(repeat)}
+    env = {"ADAPTER_TEST_REPEAT": str(repeat), "ADAPTER_TEST_EXCHANGE": exchange}
 
     res = _run(p, [scheme, "encode", e, tmp, buf], env)
     assert res.returncode == 0, res.stdout + res.stderr
@@ -78,6 +86,7 @@ def test_adapter_slot_encode_and_rebuild(oracle, tmp_path, scheme, p, e, lost, b
         os.unlink(reds[r])
     res = _run(p, [scheme, "rebuild", e, tmp, buf] + lost, env)
     assert res.returncode == 0, res.stdout + res.stderr
+    assert f"rebuild exchange {'host' if exchange == 'auto' else exchange}" in res.stdout, res.stdout
     for r in lost:
         for path, size in files[r]:
             assert os.path.getsize(path) == size
@@ -86,8 +95,9 @@ def test_adapter_slot_encode_and_rebuild(oracle, tmp_path, scheme, p, e, lost, b
         assert np.array_equal(blob[header[r]:header[r] + e * chunk], want[r]), r
 
 
+@pytest.mark.parametrize("exchange", ["auto", "sharded-mpi"])
 @pytest.mark.parametrize("scheme", ["rs", "xor"])
-def test_adapter_short_survivor_file_fails_every_rank(oracle, tmp_path, scheme):
+def test_adapter_short_survivor_file_fails_every_rank(oracle, tmp_path, scheme, exchange):
     """A survivor's data file shorter than its recorded size makes
     redset_lofi_pread fail (as redset_read_attempt's short read does,
     src/redset_lofi.c:74-77); through the adapter that member's slot returns
@@ -114,6 +124,6 @@ def test_adapter_short_survivor_file_fails_every_rank(oracle, tmp_path, scheme):
     assert sum(s for _, s in files[big]) > (d - 1) * chunk
     for path, _ in files[big]:
         os.truncate(path, 0)
-    res = _run(p, [scheme, "rebuild", e, tmp, 65536] + lost)
+    res = _run(p, [scheme, "rebuild", e, tmp, 65536] + lost, {"ADAPTER_TEST_EXCHANGE": exchange})
     assert res.returncode != 0
     assert "slot failed" in res.stderr

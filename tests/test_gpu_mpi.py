@@ -36,9 +36,26 @@ def _have():
     return os.path.exists(RANK_TEST)
 
 
-def _mpirun(np_, args, timeout=300):
+def _mpirun(np_, args, timeout=300, env=None):
     cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", RANK_TEST] + [str(a) for a in args]
-    return run_group(cmd, timeout)
+    return run_group(cmd, timeout, env={**os.environ, **(env or {})})
+
+
+# the multi-rank rebuild's exchange (include/redset_hip_mpi.h): "auto" picks
+# RCCL over xGMI when every member owns a GPU of one node -- on the test box
+# the members share one GPU, so auto must take the host path --, and
+# "sharded-mpi" runs the same sharded plan (gather column slices, gf_mac on
+# every GPU, return) over the MPI transport with device buffers
+EXCHANGES = ["auto", "sharded-mpi"]
+
+
+def _exchange_env(exchange):
+    return {"RANK_TEST_EXCHANGE": exchange}
+
+
+def _check_exchange(res, exchange):
+    used = "host" if exchange == "auto" else exchange
+    assert f"rebuild exchange {used}" in res.stdout, res.stdout
 
 
 def _setup(tmp, p, d, rng, maxsize):
@@ -72,9 +89,10 @@ def _logical(fl, total):
     return out
 
 
+@pytest.mark.parametrize("exchange", EXCHANGES)
 @pytest.mark.parametrize("scheme,p,e,lost,buf", [("rs", 6, 2, [1, 4], 65536), ("rs", 5, 3, [0, 2, 4], 40000),
                                                   ("xor", 4, 1, [2], 50000)])
-def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf):
+def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf, exchange):
     if not _have():
         pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
     tmp = str(tmp_path)
@@ -104,8 +122,9 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf):
         for path, _ in files[r]:
             os.unlink(path)
         os.unlink(reds[r])
-    res = _mpirun(p, [scheme, "rebuild", e, tmp, buf] + lost)
+    res = _mpirun(p, [scheme, "rebuild", e, tmp, buf] + lost, env=_exchange_env(exchange))
     assert res.returncode == 0, res.stdout + res.stderr
+    _check_exchange(res, exchange)
     for r in lost:
         for path, size in files[r]:
             assert os.path.getsize(path) == size
@@ -122,6 +141,11 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf):
     ("xor", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2"}),
     ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2"}),  # the root runs the GPU work
     ("xor", "rebuild", {"RANK_TEST_FAIL_READ": "0"}),
+    # the sharded exchange: every member's state is agreed on before each
+    # window's exchange, so one member's error stops all of them
+    ("rs", "rebuild", {"RANK_TEST_FAIL_READ": "3", "RANK_TEST_EXCHANGE": "sharded-mpi"}),
+    ("rs", "rebuild", {"RANK_TEST_FAIL_READ": "0", "RANK_TEST_EXCHANGE": "sharded-mpi"}),
+    ("xor", "rebuild", {"RANK_TEST_FAIL_READ": "1", "RANK_TEST_EXCHANGE": "sharded-mpi"}),
 ])
 def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme, op, env):
     """One member's I/O or device error in the middle of the loop: that member
@@ -185,7 +209,8 @@ def test_mpi_sharded_gpu(np_, p, e, chunk, lost, mode):
     assert res.stdout.count("rebuild gather") == np_
 
 
-def test_mpi_config0_xor_4_ranks_16MiB(oracle, tmp_path):
+@pytest.mark.parametrize("exchange", EXCHANGES)
+def test_mpi_config0_xor_4_ranks_16MiB(oracle, tmp_path, exchange):
     """BASELINE.json configs[0] at its own shape through the drop-in per-rank
     XOR backend: 4 MPI ranks, one 16 MiB file each (chunk = ceil(16 MiB / 3),
     src/redset_xor.c's rule), 1 MiB MPI buffer; encode, lose rank 2, rebuild."""
@@ -213,8 +238,9 @@ def test_mpi_config0_xor_4_ranks_16MiB(oracle, tmp_path):
     crc = oracle.crc32(lofi[2][:size])
     os.unlink(files[2][0][0])
     os.unlink(reds[2])
-    res = _mpirun(p, ["xor", "rebuild", e, tmp, 1 << 20, 2])
+    res = _mpirun(p, ["xor", "rebuild", e, tmp, 1 << 20, 2], env=_exchange_env(exchange))
     assert res.returncode == 0, res.stdout + res.stderr
+    _check_exchange(res, exchange)
     assert os.path.getsize(files[2][0][0]) == size
     assert oracle.crc32(np.fromfile(files[2][0][0], dtype=np.uint8)) == crc
     assert np.array_equal(np.fromfile(reds[2], dtype=np.uint8)[4096:], want[2])
@@ -244,8 +270,9 @@ def test_mpi_sharded_gpu_random(seed):
     assert res.stdout.count("rebuild gather") == np_
 
 
+@pytest.mark.parametrize("exchange", EXCHANGES)
 @pytest.mark.parametrize("scheme,p,e,lost", [("rs", 6, 2, [1, 4]), ("xor", 5, 1, [3])])
-def test_mpi_rank_backends_repeated_calls(oracle, tmp_path, scheme, p, e, lost):
+def test_mpi_rank_backends_repeated_calls(oracle, tmp_path, scheme, p, e, lost, exchange):
     """Three backend calls per process (RANK_TEST_REPEAT=3): the second and
     third run on the scratch and stream the first left in the process-wide
     cache (dirty buffers), and must write the same bytes."""
@@ -277,8 +304,9 @@ def test_mpi_rank_backends_repeated_calls(oracle, tmp_path, scheme, p, e, lost):
         os.unlink(reds[r])
     cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST, scheme, "rebuild", str(e), tmp, "32768"] + \
         [str(x) for x in lost]
-    res = run_group(cmd, 120, env=env)
+    res = run_group(cmd, 120, env={**env, **_exchange_env(exchange)})
     assert res.returncode == 0 and "call 3 of 3" in res.stdout, res.stdout + res.stderr
+    _check_exchange(res, exchange)
     for r in lost:
         for path, _ in files[r]:
             assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
@@ -321,8 +349,10 @@ def test_mpi_rank_backends_random(oracle, tmp_path, seed):
         for path, _ in files[r]:
             os.unlink(path)
         os.unlink(reds[r])
-    res = _mpirun(p, [scheme, "rebuild", e, tmp, buf] + lost, timeout=120)
-    assert res.returncode == 0, (scheme, p, e, buf, lost, res.stdout + res.stderr)
+    exchange = EXCHANGES[seed % 2]
+    res = _mpirun(p, [scheme, "rebuild", e, tmp, buf] + lost, timeout=120, env=_exchange_env(exchange))
+    assert res.returncode == 0, (scheme, p, e, buf, lost, exchange, res.stdout + res.stderr)
+    _check_exchange(res, exchange)
     for r in lost:
         for path, size in files[r]:
             assert os.path.getsize(path) == size

@@ -63,3 +63,43 @@ def test_sharded_plan_random_shapes_and_placements(oracle, seed):
     res = run_group(cmd, 120, env={**os.environ, "SHARDED_TEST_SEED": str(seed)}, cwd="/tmp")
     assert res.returncode == 0, (np_, p, e, chunk, lost, res.stdout + res.stderr)
     assert res.stdout.count("rebuild gather") == np_
+
+
+@pytest.mark.parametrize("np_,p,chunk,root", [
+    (2, 8, 3001, 3),     # configs[1]'s shape, small chunk
+    (4, 4, 4096, 0),     # configs[0]'s set size
+    (3, 5, 1, 4),        # one-byte chunk
+    (4, 9, 777, 8),
+    (1, 6, 500, 2),
+])
+def test_xor_sharded_plan_over_mpi_matches_oracle(oracle, np_, p, chunk, root):
+    """XOR sets through the same planner (redset_hip_xor_sharded_plan): the
+    encode gathers every member's p - 1 logical-file segments, the rebuild
+    every survivor's every cell (in place of the reference's pipelined reduce
+    to the lost member, src/redset_xor.c:466-524); parity and the rebuilt
+    member against the oracle's XOR (src/redset_xor.c:220-295,
+    src/redset_xor_serial.c:161-275)."""
+    if not _have():
+        pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", DRIVER, str(p), "1", str(chunk), str(root)]
+    res = run_group(cmd, 120, env={**os.environ, "SHARDED_TEST_SCHEME": "xor"}, cwd="/tmp")
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert res.stdout.count("rebuild gather") == np_
+
+
+@pytest.mark.parametrize("seed", range(8))
+def test_xor_sharded_plan_random(oracle, seed):
+    if not _have():
+        pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
+    import numpy as np
+
+    rng = np.random.default_rng(7000 + seed)
+    np_ = int(rng.integers(1, 5))
+    p = int(rng.integers(2, 20))
+    chunk = int(rng.choice([1, 255, 257, int(rng.integers(2, 5000))]))
+    root = int(rng.integers(0, p))
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", DRIVER, str(p), "1", str(chunk), str(root)]
+    env = {**os.environ, "SHARDED_TEST_SCHEME": "xor", "SHARDED_TEST_SEED": str(seed)}
+    res = run_group(cmd, 120, env=env, cwd="/tmp")
+    assert res.returncode == 0, (np_, p, chunk, root, res.stdout + res.stderr)
+    assert res.stdout.count("rebuild gather") == np_

@@ -74,6 +74,19 @@ enum {
 int redset_hip_rank_set_exchange(int mode);
 int redset_hip_rank_last_exchange(void);
 
+/* What the calling thread's last backend call moved and where it waited
+ * (one member's view): bytes read from the logical file and the redundancy
+ * file, sent and received over MPI (or, sharded, over the exchange's
+ * transport), copied to and from the GPU, written; and the seconds its host
+ * thread spent blocked in file I/O, in MPI waits and waiting for the GPU
+ * (copies, kernels, a sharded exchange) -- at most the whole call. */
+typedef struct {
+  double seconds;
+  double read_seconds, mpi_seconds, gpu_seconds, write_seconds;
+  unsigned long long read_bytes, sent_bytes, recv_bytes, h2d_bytes, d2h_bytes, write_bytes;
+} redset_hip_rank_stats;
+int redset_hip_rank_last_stats(redset_hip_rank_stats* out);
+
 /* The backends above keep a successful call's pinned host buffers, device
  * buffers and stream for the next call (at most 256 MiB pinned, 1 GiB of
  * device memory); REDSET_HIP_SCRATCH_CACHE=0 allocates and frees per call

@@ -23,6 +23,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 #include <unistd.h>
 
 #define DEFAULT_BUF ((size_t) 1 << 20) /* redset_mpi_buf_size default, src/redset.c:45 */
@@ -40,6 +41,64 @@ static int fail(const char* fmt, ...) {
 }
 
 static size_t min_sz(size_t a, size_t b) { return a < b ? a : b; }
+
+/* ---- per-call accounting (redset_hip_rank_last_stats) -------------------- */
+/* What a backend call moved and where its host thread waited: the time
+ * blocked in logical-file / redundancy-file I/O, in MPI waits, and on the
+ * GPU's copies, kernels and (sharded) exchanges. The phases overlap only
+ * across the host/device boundary, so their sum is at most the call. */
+static __thread redset_hip_rank_stats g_stats;
+
+static double now_s(void) {
+  struct timespec t;
+  clock_gettime(CLOCK_MONOTONIC, &t);
+  return (double) t.tv_sec + 1e-9 * (double) t.tv_nsec;
+}
+
+int redset_hip_rank_last_stats(redset_hip_rank_stats* out) {
+  if (!out) return fail("rank_last_stats: null argument");
+  *out = g_stats;
+  return REDSET_SUCCESS;
+}
+
+static double stats_begin(void) {
+  memset(&g_stats, 0, sizeof(g_stats));
+  return now_s();
+}
+static int stats_end(double t0, int rc) {
+  g_stats.seconds = now_s() - t0;
+  return rc;
+}
+
+/* the logical file (index = segment) */
+static int io_read(const redset_hip_io* io, int seg, unsigned long long off, size_t len, void* dst) {
+  const double t0 = now_s();
+  const int rc = io->read(io->ctx, 0, REDSET_HIP_CELL_DATA, seg, off, len, dst);
+  g_stats.read_seconds += now_s() - t0;
+  g_stats.read_bytes += len;
+  return rc;
+}
+static int io_write(const redset_hip_io* io, int seg, unsigned long long off, size_t len, const void* src) {
+  if (!io->write) return -1;
+  const double t0 = now_s();
+  const int rc = io->write(io->ctx, 0, REDSET_HIP_CELL_DATA, seg, off, len, src);
+  g_stats.write_seconds += now_s() - t0;
+  g_stats.write_bytes += len;
+  return rc;
+}
+static void isend(const void* buf, int n, int peer, int tag, MPI_Comm comm, MPI_Request* req) {
+  g_stats.sent_bytes += (unsigned long long) n;
+  MPI_Isend(buf, n, MPI_BYTE, peer, tag, comm, req);
+}
+static void irecv(void* buf, int n, int peer, int tag, MPI_Comm comm, MPI_Request* req) {
+  g_stats.recv_bytes += (unsigned long long) n;
+  MPI_Irecv(buf, n, MPI_BYTE, peer, tag, comm, req);
+}
+static void mpi_waitall(int k, MPI_Request* req) {
+  const double t0 = now_s();
+  mpi_waitall(k, req);
+  g_stats.mpi_seconds += now_s() - t0;
+}
 
 /* ---- page-locked host + device scratch and one stream ------------------- */
 /*
@@ -186,10 +245,12 @@ void redset_hip_rank_scratch_release(void) {
 }
 
 static int h2d(scratch* S, void* dst, const void* src, size_t n) {
+  g_stats.h2d_bytes += n;
   return hipMemcpyAsync(dst, src, n, hipMemcpyHostToDevice, S->stream) == hipSuccess ? 0 : fail("H2D copy failed");
 }
 
 static int d2h(scratch* S, void* dst, const void* src, size_t n) {
+  g_stats.d2h_bytes += n;
   return hipMemcpyAsync(dst, src, n, hipMemcpyDeviceToHost, S->stream) == hipSuccess ? 0 : fail("D2H copy failed");
 }
 
@@ -198,29 +259,43 @@ static int d2h(scratch* S, void* dst, const void* src, size_t n) {
  * redset_write_attempt, src/redset_io.c:234-310) --------------------------- */
 
 static int pread_full(int fd, void* buf, size_t n, off_t off) {
+  const double t0 = now_s();
+  g_stats.read_bytes += n;
   char* p = (char*) buf;
+  int rc = 0;
   while (n) {
     ssize_t k = pread(fd, p, n, off);
     if (k < 0 && errno == EINTR) continue;
-    if (k <= 0) return -1;
+    if (k <= 0) {
+      rc = -1;
+      break;
+    }
     p += k;
     n -= (size_t) k;
     off += k;
   }
-  return 0;
+  g_stats.read_seconds += now_s() - t0;
+  return rc;
 }
 
 static int pwrite_full(int fd, const void* buf, size_t n, off_t off) {
+  const double t0 = now_s();
+  g_stats.write_bytes += n;
   const char* p = (const char*) buf;
+  int rc = 0;
   while (n) {
     ssize_t k = pwrite(fd, p, n, off);
     if (k < 0 && errno == EINTR) continue;
-    if (k <= 0) return -1;
+    if (k <= 0) {
+      rc = -1;
+      break;
+    }
     p += k;
     n -= (size_t) k;
     off += k;
   }
-  return 0;
+  g_stats.write_seconds += now_s() - t0;
+  return rc;
 }
 
 /* Every member must enter the exchange loop or none may: a member whose
@@ -278,11 +353,14 @@ static int ev_record(scratch* S, hipEvent_t ev) {
   return hipEventRecord(ev, S->stream) == hipSuccess ? 0 : fail("hipEventRecord failed");
 }
 static int ev_wait(hipEvent_t ev) {
-  return hipEventSynchronize(ev) == hipSuccess ? 0 : fail("device work failed (hipEventSynchronize)");
+  const double t0 = now_s();
+  const int ok = hipEventSynchronize(ev) == hipSuccess;
+  g_stats.gpu_seconds += now_s() - t0;
+  return ok ? 0 : fail("device work failed (hipEventSynchronize)");
 }
 
-int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi,
-                              const char* chunk_file, int fd_chunk, size_t chunk_size, size_t buf_size) {
+static int rs_encode_impl(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file,
+                          int fd_chunk, size_t chunk_size, size_t buf_size) {
   int p, r, rp, e;
   off_t header;
   if (!rs || !lofi || !lofi->read) return fail("rs_encode_rank: null argument");
@@ -364,7 +442,7 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
         const int chunk_id = (r + p - 1 - s) % p;
         const int seg = redset_hip_rs_get_data_id(p, e, r, chunk_id);
         uint8_t* mine = h_send + (size_t) (s - s0) * B;
-        if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, mine) != 0) {
+        if (io_read(lofi, seg, nread, count, mine) != 0) {
           rc = fail("lofi read failed");
           memset(mine, 0, count);
         }
@@ -374,13 +452,13 @@ int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const reds
         const int step = p - 1 - s;
         for (int i = 0; i < e; ++i) {
           const int dist = p - step + i;
-          MPI_Irecv(h_recv[bb] + ((size_t) (s - s0) * e + i) * B, (int) count, MPI_BYTE, (r + dist) % p, s - s0,
+          irecv(h_recv[bb] + ((size_t) (s - s0) * e + i) * B, (int) count, (r + dist) % p, s - s0,
                     comm, &req[k++]);
-          MPI_Isend(h_send + (size_t) (s - s0) * B, (int) count, MPI_BYTE, (r - dist + p) % p, s - s0, comm,
+          isend(h_send + (size_t) (s - s0) * B, (int) count, (r - dist + p) % p, s - s0, comm,
                     &req[k++]);
         }
       }
-      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+      mpi_waitall(k, req);
       ++wcount;
       if (dev_failed) continue;
       /* the window's gs*e slices: one H2D, one kernel per slot accumulating
@@ -446,6 +524,12 @@ out:
   free(ins);
   free(req);
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi,
+                              const char* chunk_file, int fd_chunk, size_t chunk_size, size_t buf_size) {
+  const double t0 = stats_begin();
+  return stats_end(t0, rs_encode_impl(rs, comm, lofi, chunk_file, fd_chunk, chunk_size, buf_size));
 }
 
 /* ---- RS decode (replaces redset_reedsolomon_decode, src/redset_reedsolomon.c:570-785) */
@@ -525,7 +609,7 @@ static int rs_decode_host(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
         int bad;
         if (enc < p) {
           const int seg = redset_hip_rs_get_data_id(p, e, r, c);
-          bad = lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, nread, count, mine) != 0;
+          bad = io_read(lofi, seg, nread, count, mine) != 0;
           if (bad) rc = fail("lofi read failed");
         } else {
           const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) nread;
@@ -534,21 +618,23 @@ static int rs_decode_host(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
         }
         if (bad) memset(mine, 0, count);
       }
+      /* stripe r's used cells land packed, input j at j * B, so one copy of
+       * ncols cells moves them to the GPU */
       int k = 0;
-      for (int j = 0; j < ncols; ++j)
-        if (cols[j] != r)
-          MPI_Irecv(h_cells[bb] + (size_t) cols[j] * B, (int) count, MPI_BYTE, cols[j], TAG_RING, comm, &req[k++]);
+      for (int j = 0; j < ncols; ++j) {
+        if (cols[j] != r) irecv(h_cells[bb] + (size_t) j * B, (int) count, cols[j], TAG_RING, comm, &req[k++]);
+        else memcpy(h_cells[bb] + (size_t) j * B, h_send + (size_t) r * B, count);
+      }
       for (int c = 0; c < p; ++c)
         if (c != r && send_to[c])
-          MPI_Isend(h_send + (size_t) c * B, (int) count, MPI_BYTE, c, TAG_RING, comm, &req[k++]);
-      if (send_to[r]) memcpy(h_cells[bb] + (size_t) r * B, h_send + (size_t) r * B, count);
-      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+          isend(h_send + (size_t) c * B, (int) count, c, TAG_RING, comm, &req[k++]);
+      mpi_waitall(k, req);
       /* enqueue this slice's solve; it runs while the previous slice is gathered */
       if (!dev_failed) {
-        for (int k = 0; k < ncols; ++k) ins[k] = d_cells[bb] + (size_t) cols[k] * B;
+        for (int k = 0; k < ncols; ++k) ins[k] = d_cells[bb] + (size_t) k * B;
         for (int i = 0; i < missing; ++i) outs[i] = d_out[bb] + (size_t) i * B;
         int grc = injected_device_failure(comm);
-        if (!grc) grc = h2d(&S, d_cells[bb], h_cells[bb], (size_t) p * B);
+        if (!grc && ncols > 0) grc = h2d(&S, d_cells[bb], h_cells[bb], (size_t) ncols * B);
         if (!grc && ncols > 0) grc = redset_hip_gf_combine(ins, ncols, outs, missing, coef, count, 0, S.stream);
         if (!grc) grc = d2h(&S, h_out[bb], d_out[bb], (size_t) missing * B);
         if (!grc) grc = ev_record(&S, ev_done[bb]);
@@ -569,12 +655,12 @@ static int rs_decode_host(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
       if (need_rebuild)
         for (int step = 0; step < p; ++step) {
           const int lhs = (r - step + p) % p;
-          MPI_Irecv(h_gather + (size_t) lhs * B, (int) prev_count, MPI_BYTE, lhs, TAG_GATHER, comm, &req[k++]);
+          irecv(h_gather + (size_t) lhs * B, (int) prev_count, lhs, TAG_GATHER, comm, &req[k++]);
         }
       for (int i = 0; i < missing; ++i)
-        MPI_Isend(h_out[prev_b] + (size_t) i * B, (int) prev_count, MPI_BYTE, rebuild_ranks[i], TAG_GATHER, comm,
+        isend(h_out[prev_b] + (size_t) i * B, (int) prev_count, rebuild_ranks[i], TAG_GATHER, comm,
                   &req[k++]);
-      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+      mpi_waitall(k, req);
       if (need_rebuild) { /* :736-765 */
         for (int step = 0; step < p; ++step) {
           const int lhs = (r - step + p) % p;
@@ -582,7 +668,7 @@ static int rs_decode_host(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
           const uint8_t* cell = h_gather + (size_t) lhs * B;
           if (enc < p) {
             const int seg = redset_hip_rs_get_data_id(p, e, r, lhs);
-            if (!lofi->write || lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, seg, prev_nread, prev_count, cell) != 0)
+            if (io_write(lofi, seg, prev_nread, prev_count, cell) != 0)
               rc = fail("lofi write failed");
           } else {
             const off_t off = header + (off_t) (enc - p) * (off_t) chunk_size + (off_t) prev_nread;
@@ -614,8 +700,8 @@ out:
 
 /* ---- XOR encode (replaces redset_xor_encode, src/redset_xor.c:220-295) */
 
-int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
-                               size_t chunk_size, size_t buf_size) {
+static int xor_encode_impl(MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
+                           size_t chunk_size, size_t buf_size) {
   int p, r;
   off_t header;
   if (!lofi || !lofi->read) return fail("xor_encode_rank: null argument");
@@ -660,15 +746,15 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
        * every other member's cell of stripe r; exchange those cells directly */
       for (int t = 0; t < p; ++t) {
         if (t == r) continue;
-        if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, t), nread, count,
+        if (io_read(lofi, xor_segment(r, t), nread, count,
                        h_send + (size_t) t * B) != 0) {
           rc = fail("lofi read failed");
           memset(h_send + (size_t) t * B, 0, count);
         }
-        MPI_Irecv(h_recv[bb] + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
-        MPI_Isend(h_send + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
+        irecv(h_recv[bb] + (size_t) t * B, (int) count, t, 0, comm, &req[k++]);
+        isend(h_send + (size_t) t * B, (int) count, t, 0, comm, &req[k++]);
       }
-      MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+      mpi_waitall(k, req);
       if (!dev_failed) {
         int nin = 0;
         for (int t = 0; t < p; ++t)
@@ -705,6 +791,12 @@ out:
   free(ins);
   free(req);
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
+                               size_t chunk_size, size_t buf_size) {
+  const double t0 = stats_begin();
+  return stats_end(t0, xor_encode_impl(comm, lofi, chunk_file, fd_chunk, chunk_size, buf_size));
 }
 
 /* ---- XOR decode (replaces redset_xor_decode, src/redset_xor.c:441-531) */
@@ -747,14 +839,17 @@ static int xor_decode_host(MPI_Comm comm, int p, int r, int root, const redset_h
         uint8_t* mine = h_cells[0] + (size_t) r * B;
         int bad;
         if (c != r) {
-          bad = lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(r, c), nread, count, mine) != 0;
+          bad = io_read(lofi, xor_segment(r, c), nread, count, mine) != 0;
           if (bad) rc = fail("lofi read failed");
         } else {
           bad = pread_full(fd_chunk, mine, count, header + (off_t) nread) != 0;
           if (bad) rc = fail("read %s failed", chunk_file);
         }
         if (bad) memset(mine, 0, count);
+        const double t0 = now_s();
         MPI_Send(mine, (int) count, MPI_BYTE, root, 0, comm);
+        g_stats.mpi_seconds += now_s() - t0;
+        g_stats.sent_bytes += count;
         continue;
       }
       if (r != root) continue;
@@ -763,8 +858,8 @@ static int xor_decode_host(MPI_Comm comm, int p, int r, int root, const redset_h
          * unit n-2 was written (below, during unit n-1) */
         int k = 0;
         for (int t = 0; t < p; ++t)
-          if (t != root) MPI_Irecv(h_cells[bb] + (size_t) t * B, (int) count, MPI_BYTE, t, 0, comm, &req[k++]);
-        MPI_Waitall(k, req, MPI_STATUSES_IGNORE);
+          if (t != root) irecv(h_cells[bb] + (size_t) t * B, (int) count, t, 0, comm, &req[k++]);
+        mpi_waitall(k, req);
         if (!dev_failed) {
           int nin = 0;
           for (int t = 0; t < p; ++t)
@@ -785,7 +880,7 @@ static int xor_decode_host(MPI_Comm comm, int p, int r, int root, const redset_h
           rc = REDSET_FAILURE;
           dev_failed = 1;
         } else if (prev_c != root) {
-          if (!lofi->write || lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, xor_segment(root, prev_c), prev_nread,
+          if (io_write(lofi, xor_segment(root, prev_c), prev_nread,
                                           prev_count, h_out[prev_b]) != 0)
             rc = fail("lofi write failed");
         } else if (pwrite_full(fd_chunk, h_out[prev_b], prev_count, header + (off_t) prev_nread) != 0) {
@@ -1017,7 +1112,7 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
     const size_t off = n * win, len = n + 1 == nwin ? tail : win;
     if (n < nwin) {
       /* buffers b were last used by window n - 2, written at window n - 1 */
-      if (n >= 2 && !rc && hipEventSynchronize(ev[b]) != hipSuccess) rc = fail("device work failed");
+      if (n >= 2 && !rc && ev_wait(ev[b])) rc = REDSET_FAILURE;
       /* the plan of buffers b for a whole window, or for the tail window
        * (planning is local: no communication, every member the same) */
       redset_hip_sharded** P = &plan[b][len != win];
@@ -1031,14 +1126,16 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
         if (!want[x]) continue;
         uint8_t* dst = img + (size_t) x * WW;
         if (x < d) {
-          if (lofi->read(lofi->ctx, 0, REDSET_HIP_CELL_DATA, x, off, len, dst) != 0) rc = fail("lofi read failed");
+          if (io_read(lofi, x, off, len, dst) != 0) rc = fail("lofi read failed");
         } else if (pread_full(fd_chunk, dst, len, header + (off_t) (x - d) * (off_t) chunk_size + (off_t) off) != 0) {
           rc = fail("read %s failed", chunk_file);
         }
       }
       /* every member's state before the exchange: one failure stops all */
       int ok = rc == 0, all = 0;
+      const double ta = now_s();
       if (MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_LAND, comm) != MPI_SUCCESS) rc = fail("MPI_Allreduce failed");
+      g_stats.mpi_seconds += now_s() - ta;
       if (!all) {
         if (!rc) rc = fail("a peer's read or device step failed");
         stopped = 1;
@@ -1052,14 +1149,21 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
         if (hipMemcpy2DAsync(dst, dpitch, img + (size_t) x * WW, W, W, (size_t) world, hipMemcpyHostToDevice, s) !=
             hipSuccess)
           rc = fail("H2D copy failed");
+        g_stats.h2d_bytes += WW;
       }
       if (!rc && redset_hip_sharded_execute(*P, s) != 0) rc = REDSET_FAILURE;
+      redset_hip_sharded_info info;
+      if (!rc && redset_hip_sharded_get_info(*P, &info) == 0) {
+        g_stats.sent_bytes += info.gather_bytes_sent + info.return_bytes_sent;
+        g_stats.recv_bytes += info.gather_bytes_recv + info.return_bytes_recv;
+      }
       for (int x = 0; x < ncell && !rc && need_rebuild; ++x) {
         const uint8_t* src = x < d ? hd[b] + (size_t) x * W : hp[b] + (size_t) (x - d) * W;
         const size_t spitch = (size_t) (x < d ? d : e) * W;
         if (hipMemcpy2DAsync(img + (size_t) x * WW, W, src, spitch, W, (size_t) world, hipMemcpyDeviceToHost, s) !=
             hipSuccess)
           rc = fail("D2H copy failed");
+        g_stats.d2h_bytes += WW;
       }
       if (!rc && hipEventRecord(ev[b], s) != hipSuccess) rc = fail("hipEventRecord failed");
     }
@@ -1067,11 +1171,11 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
     if (n >= 1 && need_rebuild && !rc) {
       const int pb = 1 - b;
       const size_t poff = (n - 1) * win, plen = n == nwin ? tail : win;
-      if (hipEventSynchronize(ev[pb]) != hipSuccess) rc = fail("device work failed");
+      if (ev_wait(ev[pb])) rc = REDSET_FAILURE;
       for (int x = 0; x < ncell && !rc; ++x) {
         const uint8_t* cell = h_img[pb] + (size_t) x * WW;
         if (x < d) {
-          if (lofi->write(lofi->ctx, 0, REDSET_HIP_CELL_DATA, x, poff, plen, cell) != 0) rc = fail("lofi write failed");
+          if (io_write(lofi, x, poff, plen, cell) != 0) rc = fail("lofi write failed");
         } else if (pwrite_full(fd_chunk, cell, plen, header + (off_t) (x - d) * (off_t) chunk_size + (off_t) poff) != 0) {
           rc = fail("write %s failed", chunk_file);
         }
@@ -1098,6 +1202,7 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
                               size_t chunk_size, size_t buf_size) {
   int p, r, rp, e;
   off_t header;
+  const double t0 = stats_begin();
   if (!rs || !lofi || !rebuild_ranks) return fail("rs_decode_rank: null argument");
   if (comm_geometry(comm, &p, &r) || redset_hip_rs_shape(rs, &rp, &e)) return REDSET_FAILURE;
   if (p != rp) return fail("communicator has %d ranks, codec %d", p, rp);
@@ -1124,13 +1229,14 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
                : decode_sharded(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
                                 header, hrc, chunk_size, B, &tr);
   redset_hip_mpi_transport_destroy(mt);
-  return rc;
+  return stats_end(t0, rc);
 }
 
 int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
                                int fd_chunk, size_t chunk_size, size_t buf_size) {
   int p, r;
   off_t header;
+  const double t0 = stats_begin();
   if (!lofi || !lofi->read) return fail("xor_decode_rank: null argument");
   if (comm_geometry(comm, &p, &r)) return REDSET_FAILURE;
   if (p < 2) return fail("XOR needs at least 2 ranks");
@@ -1153,7 +1259,7 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
                : decode_sharded(NULL, comm, p, r, 1, 1, &root, r == root, lofi, chunk_file, fd_chunk, header, hrc,
                                 chunk_size, B, &tr);
   redset_hip_mpi_transport_destroy(mt);
-  return rc;
+  return stats_end(t0, rc);
 }
 
 /* ---- MPI transport of the sharded path (include/redset_hip_mpi.h) ------- */

@@ -377,9 +377,22 @@ class ShardedSetRunner:
                 "rebuild": f"{tname}: grouped P2P, decode inputs' slices in, rebuilt slices back to their hosts "
                            "(redset_hip_rs_sharded_plan)"}
         phases = self.phase_ms() if self.timing else None
+        ops = ["encode", "rebuild"] if op == "step" else [op]
+        msgs = {}
+        for o in ops:
+            if o in self._plans:
+                i = self.info(o)
+                # peer messages this GPU sends per execute after the planner's
+                # row merging (every set's gather and return is an exchange
+                # of its own), and their size range
+                msgs[o] = {"gather_messages": i["gather_messages"], "return_messages": i["return_messages"],
+                           "gather_msg_bytes": [i["gather_msg_min"], i["gather_msg_max"]],
+                           "return_msg_bytes": [i["return_msg_min"], i["return_msg_max"]],
+                           "exchanges": 2 * self.world}
         out = {
             "exchange": {
                 "bytes_sent_per_gpu_per_step": self.exchanged_bytes(op),
+                "messages_per_gpu": msgs,
                 "column_slice_bytes": self.W,
                 "collective": coll.get(op, coll["encode"] + "; " + coll["rebuild"]),
                 "phase_ms_rank0": phases,

@@ -66,6 +66,26 @@ static const char* exchange_name(int m) {
                                                  : "none";
 }
 
+/* the last call's accounting (redset_hip_rank_last_stats), max and sum over
+ * the ranks, as one JSON line from rank 0 (tools/rank_bench.py reads it) */
+static void print_stats(int rank, const char* tag) {
+  static const char* names[] = {"seconds", "read_seconds", "mpi_seconds", "gpu_seconds", "write_seconds",
+                                "read_bytes", "sent_bytes", "recv_bytes", "h2d_bytes", "d2h_bytes", "write_bytes"};
+  redset_hip_rank_stats st;
+  memset(&st, 0, sizeof(st));
+  (void) redset_hip_rank_last_stats(&st);
+  double v[11] = {st.seconds, st.read_seconds, st.mpi_seconds, st.gpu_seconds, st.write_seconds,
+                  (double) st.read_bytes, (double) st.sent_bytes, (double) st.recv_bytes, (double) st.h2d_bytes,
+                  (double) st.d2h_bytes, (double) st.write_bytes};
+  double mx[11], sm[11];
+  MPI_Reduce(v, mx, 11, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+  MPI_Reduce(v, sm, 11, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
+  if (rank != 0) return;
+  printf("rank_stats %s {", tag);
+  for (int i = 0; i < 11; ++i) printf("%s\"%s\": [%.6g, %.6g]", i ? ", " : "", names[i], mx[i], sm[i]);
+  printf("}\n");
+}
+
 int main(int argc, char** argv) {
   MPI_Init(&argc, &argv);
   int rank, ranks;
@@ -148,6 +168,7 @@ int main(int argc, char** argv) {
   MPI_Reduce(&dt, &dmax, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
   if (rank == 0) printf("rank_test: %s %s %d ranks chunk %llu buf %zu: %.4f s\n", argv[1], argv[2], ranks, chunk, buf, dmax);
   if (rank == 0 && !encode) printf("rank_test: rebuild exchange %s\n", exchange_name(redset_hip_rank_last_exchange()));
+  print_stats(rank, "first");
 
   const char* rep = getenv("RANK_TEST_REPEAT");
   const int repeat = rep && atoi(rep) > 1 ? atoi(rep) : 1;
@@ -164,6 +185,7 @@ int main(int argc, char** argv) {
     double d = MPI_Wtime() - ti, dm = 0;
     MPI_Reduce(&d, &dm, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
     if (rank == 0 && it == repeat - 1) printf("rank_test: call %d of %d (warm): %.4f s\n", it + 1, repeat, dm);
+    if (it == repeat - 1) print_stats(rank, "warm");
   }
   close(fd);
   redset_hip_fileio_destroy(files);

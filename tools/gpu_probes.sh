@@ -1,0 +1,58 @@
+#!/bin/bash
+# Measurement probes on a GPU box, each under its own time limit; results
+# under gpurun_out/<tag>/. Stops at the first step that faults / aborts /
+# times out. usage: tools/gpu_probes.sh <tag> <probe>...
+#   gloo   torch gloo P2P rate at world 2, CPU and GPU tensors (what the N>1
+#          rehearsals' callback transport pays; tools/gloo_p2p_probe.py)
+#   n2     bench.py --gpus 2 rehearsal over gloo on the one GPU
+#   rank   the per-rank slot's roofline (tools/rank_bench.py): RS(8+3) 64 MiB
+#          and configs[0] (XOR, 4 x 16 MiB files), host and sharded exchange
+#   wide   RS(16+4) (configs[4]'s stripe) device-resident: kernel stats, PMC
+#          FETCH/WRITE and SQ counters
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+TAG=${1:-probe}; shift
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+run() { # name seconds cmd...
+  local name=$1 secs=$2; shift 2
+  echo "== $name" | tee -a "$OUT/progress.txt"
+  timeout -k 10 "$secs" "$@" > "$OUT/$name.out" 2> "$OUT/$name.err"
+  local s=$?
+  echo "$name exit $s" | tee -a "$OUT/progress.txt"
+  tail -2 "$OUT/$name.out"
+  [ $s -eq 0 ] || [ $s -eq 1 ] || exit $s
+}
+for probe in "$@"; do
+  case $probe in
+    gloo)
+      run gloo_cpu 200 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29541 tools/gloo_p2p_probe.py --device cpu
+      run gloo_cuda 400 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29542 tools/gloo_p2p_probe.py --device cuda --reps 1 ;;
+    n2)
+      run n2_gloo 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
+        --master-port 29543 bench.py --gpus 2 --dist-backend gloo --chunk-mib 2 --steps 3 --warmup 1 \
+        --cpu-baseline 0 --pairs 0 ;;
+    rank)
+      for ex in host sharded-mpi; do
+        run rank_rs_64m_$ex 400 python tools/rank_bench.py --ranks 11 --encoding 3 --chunk-mib 64 --buf-mib 16 \
+          --repeat 3 --exchange $ex --dir /tmp/rank_bench_$ex
+        run rank_config0_$ex 200 python tools/rank_bench.py --scheme xor --ranks 4 --file-bytes 16777216 \
+          --buf-mib 1 --repeat 3 --exchange $ex --lost 2 --dir /tmp/rank_c0_$ex
+      done ;;
+    wide)
+      W="--ranks 20 --encoding 4 --lost 1,2,3,4 --cpu-baseline 0 --pairs 0 --xor 0"
+      run wide_bench 300 python bench.py --steps 10 --warmup 3 $W
+      run wide_stats 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/wide_prof" -o wide -- \
+        python3 bench.py --steps 10 --warmup 3 $W
+      run wide_fetch 120 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/wide_fetch" -o fetch -- \
+        python3 bench.py --steps 4 --warmup 1 $W
+      run wide_write 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d "$OUT/wide_write" -o write -- \
+        python3 bench.py --steps 4 --warmup 1 $W
+      python3 tools/pmc_traffic.py "$OUT/wide_fetch" "$OUT/wide_write" "$OUT/wide_traffic.json" > /dev/null
+      OUT=$OUT/wide_sq BENCH_ARGS="$W" timeout -k 10 400 bash tools/pmc_sq.sh > "$OUT/wide_sq.out" 2>&1
+      echo "wide_sq exit $?" | tee -a "$OUT/progress.txt" ;;
+  esac
+done
+echo "== done" | tee -a "$OUT/progress.txt"

@@ -5,7 +5,7 @@
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=${OUT:-gpurun_out/pmcsq}; mkdir -p $OUT
-B="python3 bench.py --steps 4 --warmup 1 --cpu-baseline 0 --pairs 0 --xor 0"
+B="python3 bench.py --steps 4 --warmup 1 --cpu-baseline 0 --pairs 0 --xor 0 ${BENCH_ARGS:-}"
 G1="SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_IDX_ACTIVE SQ_LDS_BANK_CONFLICT SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_INST_LDS SQ_WAIT_ANY"
 G2="SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_SCA SQ_INSTS_SALU SQ_INSTS_VMEM_WR SQ_INSTS_VMEM_RD SQ_INST_CYCLES_VMEM"
 args=()

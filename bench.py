@@ -201,6 +201,20 @@ def load_traffic(path, kernel_prefix):
         return None
 
 
+def traffic_source(path):
+    """Where the PMC bytes of `path` were measured (its _provenance block):
+    another process -- rocprofv3 must wrap the program -- of this bench,
+    usually on another box and in another session than this line's."""
+    try:
+        with open(path) as f:
+            prov = json.load(f).get("_provenance") or {}
+    except (OSError, ValueError):
+        prov = {}
+    where = ", ".join(f"{k} {prov[k]}" for k in ("session", "host", "date") if prov.get(k))
+    return (f"{os.path.relpath(path, ROOT)} ({where or 'provenance not recorded'}): rocprofv3 --pmc FETCH_SIZE / "
+            "WRITE_SIZE in separate runs of this bench, not measured in this process")
+
+
 def cell_pad(args, chunk):
     """Bytes after every cell: --cell-pad-mib, or (-1) what the library's
     recommended stride adds to the 256-B-aligned chunk (include/redset_hip.h
@@ -611,7 +625,7 @@ def main():
         "launches_per_step": {"encode": el, "rebuild": rl},
         "algorithmic_bytes_per_launch": {"encode": eb1, "rebuild": rb1, "mean": (eb + rb) // (el + rl)},
         "traffic_per_launch": {"encode": t_enc, "rebuild": t_reb},
-        "traffic_source": "profiles/traffic_latest.json (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)",
+        "traffic_source": traffic_source(args.traffic_json),
         "avg_launch_ms": {"encode": round(enc_ms / el, 4), "rebuild": round(reb_ms / rl, 4)},
     }
     result["breakdown"] = {

@@ -18,8 +18,10 @@
  * backend n times (fd repositioned after the header each time) and also
  * print the last call's time (warm: code object loaded, caches hot).
  */
+#include <execinfo.h>
 #include <fcntl.h>
 #include <hip/hip_runtime_api.h>
+#include <signal.h>
 #include <mpi.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -86,7 +88,20 @@ static void print_stats(int rank, const char* tag) {
   printf("}\n");
 }
 
+/* a crash prints where it happened (test driver diagnostics) */
+static void on_fatal(int sig) {
+  void* bt[64];
+  const int n = backtrace(bt, 64);
+  fprintf(stderr, "rank_test: signal %d\n", sig);
+  backtrace_symbols_fd(bt, n, 2);
+  signal(sig, SIG_DFL);
+  raise(sig);
+}
+
 int main(int argc, char** argv) {
+  setvbuf(stdout, NULL, _IOLBF, 0);
+  signal(SIGSEGV, on_fatal);
+  signal(SIGBUS, on_fatal);
   MPI_Init(&argc, &argv);
   int rank, ranks;
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);

@@ -12,7 +12,9 @@ import glob
 import json
 import os
 import re
+import socket
 import sys
+import time
 
 
 def per_kernel(d, counter):
@@ -43,6 +45,14 @@ def main():
             out[k] = int((2.0 * fetch[k] + write[k]) * 1024)
             out[k + ":detail"] = {"FETCH_SIZE_KiB_raw": fetch[k], "fetch_bytes_corrected": int(2 * fetch[k] * 1024),
                                   "WRITE_SIZE_KiB": write[k], "write_bytes": int(write[k] * 1024)}
+    # where these bytes were measured: the session (gpurun_out/<session>/...),
+    # the box and the date -- bench.py names them in its traffic_source
+    parts = os.path.normpath(os.path.abspath(sys.argv[1])).split(os.sep)
+    session = parts[parts.index("gpurun_out") + 1] if "gpurun_out" in parts[:-1] else os.path.basename(sys.argv[1])
+    out["_provenance"] = {"session": session, "host": socket.gethostname(),
+                          "date": time.strftime("%Y-%m-%d %H:%M:%S %Z"),
+                          "method": "rocprofv3 --pmc FETCH_SIZE and --pmc WRITE_SIZE, separate runs of "
+                                    "bench.py --steps 4 --warmup 1 on that box"}
     with open(sys.argv[3], "w") as f:
         json.dump(out, f, indent=1)
     print(json.dumps(out, indent=1))

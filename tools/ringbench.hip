@@ -17,6 +17,8 @@
 // it waits for a free slot, so every issued item is eventually published.
 // Every spin is bounded (kSpinCap); a capped spin sets an error flag.
 // Build: hipcc -O3 --offload-arch=gfx950 -o tools/ringbench tools/ringbench.hip
+//   (-DRB_NIN=16 -DRB_NOUT=4 -DRB_BLOCK=1024: the RS(16+4) stripe at the
+//   codec's block shape; the ring gets as many slots as 144 KiB of LDS hold)
 // Run: ringbench [reps] [rand]
 #include <hip/hip_runtime.h>
 
@@ -33,7 +35,17 @@
     }                                                                            \
   } while (0)
 
-constexpr int NIN = 8, NOUT = 3, kBlock = 512, kWaves = kBlock / 64;
+#ifndef RB_NIN
+#define RB_NIN 8
+#endif
+#ifndef RB_NOUT
+#define RB_NOUT 3
+#endif
+#ifndef RB_BLOCK
+#define RB_BLOCK 512
+#endif
+constexpr int NIN = RB_NIN, NOUT = RB_NOUT, kBlock = RB_BLOCK, kWaves = kBlock / 64;
+constexpr int kSlots = 144 / NIN > 16 ? 16 : 144 / NIN;  // slots of NIN KiB in 144 KiB
 constexpr unsigned kSpinCap = 1u << 24;
 
 typedef unsigned int v4u __attribute__((ext_vector_type(4)));
@@ -72,7 +84,7 @@ __device__ __forceinline__ void wait_vm() {
 __device__ __forceinline__ unsigned lds_ld(unsigned* p) { return *(lvu*) p; }
 __device__ __forceinline__ void lds_st(unsigned* p, unsigned v) { *(lvu*) p = v; }
 
-template <int L, int D, int S = 16>
+template <int L, int D, int S = kSlots>
 __global__ void __launch_bounds__(kBlock) kring(Stripe J, size_t nvec, unsigned* err) {
   static_assert(L >= 1 && L < kWaves && D >= 1 && (D - 1) * L < S, "ring shape");
   constexpr int C = kWaves - L;
@@ -126,7 +138,7 @@ __global__ void __launch_bounds__(kBlock) kring(Stripe J, size_t nvec, unsigned*
       }
       pend[npend++] = k;
       if (npend == D) {
-        wait_vm<(D - 1) * NIN>();  // the oldest item has landed
+        wait_vm<((D - 1) * NIN > 63 ? 63 : (D - 1) * NIN)>();  // the oldest item has landed (D within vmcnt: see main)
         publish_oldest();
       }
     }
@@ -248,12 +260,8 @@ int main(int argc, char** argv) {
     run("plain", [&](const Stripe& J) { kplain<<<grid, kBlock>>>(J, nvec); });
     run("ring L1 D2", [&](const Stripe& J) { kring<1, 2><<<grid, kBlock>>>(J, nvec, err); });
     run("ring L1 D3", [&](const Stripe& J) { kring<1, 3><<<grid, kBlock>>>(J, nvec, err); });
-    run("ring L1 D4", [&](const Stripe& J) { kring<1, 4><<<grid, kBlock>>>(J, nvec, err); });
-    run("ring L1 D4 S8", [&](const Stripe& J) { kring<1, 4, 8><<<grid, kBlock>>>(J, nvec, err); });
-    run("ring L1 D5", [&](const Stripe& J) { kring<1, 5><<<grid, kBlock>>>(J, nvec, err); });
-    run("ring L1 D6", [&](const Stripe& J) { kring<1, 6><<<grid, kBlock>>>(J, nvec, err); });
-    run("ring L1 D8", [&](const Stripe& J) { kring<1, 8><<<grid, kBlock>>>(J, nvec, err); });
-    run("ring L1 D8 S12", [&](const Stripe& J) { kring<1, 8, 12><<<grid, kBlock>>>(J, nvec, err); });
+    if (3 * NIN <= 63) run("ring L1 D4", [&](const Stripe& J) { kring<1, 4><<<grid, kBlock>>>(J, nvec, err); });
+    if (4 * NIN <= 63) run("ring L1 D5", [&](const Stripe& J) { kring<1, 5><<<grid, kBlock>>>(J, nvec, err); });
     run("ring L2 D2", [&](const Stripe& J) { kring<2, 2><<<grid, kBlock>>>(J, nvec, err); });
   }
   return 0;

@@ -785,7 +785,7 @@ __device__ __forceinline__ void gf_mac_stream(const GfLaunch& L) {
 }
 
 // Slow, table-free product of one 16-B position (the claimed kernel's last
-// resort, for items whose tables may not exist: see gf_mac_claimed): a dword
+// resort, for items whose tables may not exist: see claimed_sweep): a dword
 // at a time, bytes multiplied in parallel within it (shift-and-add with the
 // 0x11D reduction per byte), loops kept rolled so that it adds few registers
 // to the consumer loop it sits in
@@ -848,24 +848,69 @@ constexpr unsigned kClaimLook = 2;
 // in the window between the claimer's BYPASS check and its record would be
 // gone from the queue and computed by no one. The counters are
 // zeroed by the launcher on the stream before every launch.
-template <int NIN, int NOUT, bool ACC>
-__device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
+// The combine of a claimed launch (claimed_sweep): GF, with per-job tables
+// in two LDS buffers (gf_lds: tables first, the ring behind them), or XOR.
+template <int NIN_, int NOUT, bool ACC>
+struct GfClaim {
+  static constexpr int NIN = NIN_;
   static_assert(NIN <= 8 && 2 * NIN * kTableBytes <= kTableVecs * 16, "two jobs' tables in the table region");
   static_assert(kRingGfRows == 1, "one-row items");
-  constexpr int S = ring_slots<NIN>();
+  static constexpr bool kTables = true;
+  static constexpr int kSlots = ring_slots<NIN>();
+  static constexpr int kRingOff = kTableVecs;
+  static constexpr int kTab = NIN * kTableBytes;  // one job's tables (bytes)
+  using Launch = GfLaunch;
+  using Job = GfJob;
+  using Body = GfAcc<NOUT, ACC>;
+  typedef __attribute__((address_space(4))) const GfJob c_job;
+  static __device__ __forceinline__ v4u* lds() { return gf_lds<NIN>(); }
+  static __device__ __forceinline__ void init(Body& b, const uint32_t* lds) { b.lds = lds; }
+  static __device__ __forceinline__ void set_out(Body& b, const c_job* J) {
+#pragma unroll
+    for (int j = 0; j < NOUT; ++j) b.out[j] = (g_u4*) (J->out[j]);
+  }
+  // job j's tables into buffer j & 1: the whole block (first job), or the loader wave
+  static __device__ __forceinline__ void first_tables(uint32_t* lds, const c_job* J, unsigned j) {
+    for (int e = threadIdx.x; e < NIN * 32; e += blockDim.x) {
+      const int i = e >> 5, h = (e >> 4) & 1, n = e & 15;
+      const uint32_t x = static_cast<uint32_t>(n) << (4 * h);
+      uint32_t v = 0;
+#pragma unroll
+      for (int o = 0; o < NOUT; ++o) v |= gf_mul_dev(J->coef[o][i], x) << (8 * o);
+      lds[((j & 1) * kTab + i * kTableBytes + (h ? kHiBase + n * kHiStride : n * 4)) / 4] = v;
+    }
+  }
+  static __device__ __forceinline__ void next_tables(uint32_t* lds, const c_job* J, unsigned j, int lane) {
+    build_tables_wave<NIN, NOUT>(lds, (j & 1) * kTab, J, lane);
+  }
+  static __device__ __forceinline__ void combine(Body& b, const v4u (&x)[NIN], unsigned job, size_t v) {
+    b.begin();
+    if (job & 1) b.template add<0, NIN, kTab>(x);
+    else b.template add<0, NIN, 0>(x);
+    b.finish(v);
+  }
+  static __device__ __forceinline__ void slow(const c_job* J, g_cu4* const (&in)[NIN], size_t v) {
+    gf_mac_vec_slow<NIN, NOUT, ACC>(J, in, v);
+  }
+};
+
+template <typename Pol>
+__device__ __forceinline__ void claimed_sweep(const typename Pol::Launch& L) {
+  constexpr int NIN = Pol::NIN;
+  constexpr int S = Pol::kSlots;
   constexpr int D = ring_depth<NIN, 1, kRingRowsInFlight>();
   constexpr int C = kBlock / 64 - 2;  // consumer waves
-  constexpr int kTab = NIN * kTableBytes;
   constexpr unsigned B = kClaimBatch;
   constexpr unsigned kLook = kClaimLook;
   constexpr unsigned NB = 32;
   static_assert(C >= 1 && NB * B >= S + (kLook + 1) * B, "batch ring");
-  typedef __attribute__((address_space(4))) const GfJob c_job;
+  static_assert(D - 1 < S && (D - 1) * NIN <= 63, "ring depth");
+  typedef __attribute__((address_space(4))) const typename Pol::Job c_job;
   const c_job* const jobs = (const c_job*) (L.jobs + L.job0);
   const unsigned cap = RING_SPIN_CAP(L);
-  v4u* const smem = gf_lds<NIN>();
+  v4u* const smem = Pol::lds();
   uint32_t* const lds = reinterpret_cast<uint32_t*>(smem);
-  v4u* const ring = smem + kTableVecs;
+  v4u* const ring = smem + Pol::kRingOff;
   __shared__ unsigned full[S], freed[S], prog[C], bbase[NB];
   __shared__ unsigned bypass, tab_job, seq_end, nclaimed, claim_end, lbatch, first, claimer_done;
 
@@ -892,17 +937,7 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
   }
   __syncthreads();
   const unsigned b0 = first;
-  if (b0 < total) {
-    const unsigned job0 = b0 / RQ;
-    for (int e = threadIdx.x; e < NIN * 32; e += blockDim.x) {
-      const int i = e >> 5, h = (e >> 4) & 1, n = e & 15;
-      const uint32_t x = static_cast<uint32_t>(n) << (4 * h);
-      uint32_t v = 0;
-#pragma unroll
-      for (int j = 0; j < NOUT; ++j) v |= gf_mul_dev(jobs[job0].coef[j][i], x) << (8 * j);
-      lds[((job0 & 1) * kTab + i * kTableBytes + (h ? kHiBase + n * kHiStride : n * 4)) / 4] = v;
-    }
-  }
+  if (b0 < total) Pol::first_tables(lds, jobs + b0 / RQ, b0 / RQ);
   if (threadIdx.x < S) full[threadIdx.x] = 0, freed[threadIdx.x] = 0;
   if (threadIdx.x < C) prog[threadIdx.x] = threadIdx.x;
   if (threadIdx.x == 0) {
@@ -964,16 +999,18 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
           last_end[job & 1] = p;
           job = bj;
           const unsigned T = last_end[job & 1];
-          if (!past(T)) {
+          if (Pol::kTables && !past(T)) {
             ring_wait_vm<0>();
             while (pub < p) publish();
             unsigned spins = 0;
             while (!past(T) && ++spins < kRingHangCap) __builtin_amdgcn_s_sleep(1);
             if (spins >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
           }
-          build_tables_wave<NIN, NOUT>(lds, (job & 1) * kTab, jobs + job, lane);
-          asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-          if (lane == 0) ring_flag_st(&tab_job, job);
+          if constexpr (Pol::kTables) {
+            Pol::next_tables(lds, jobs + job, job, lane);
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            if (lane == 0) ring_flag_st(&tab_job, job);
+          }
 #pragma unroll
           for (int i = 0; i < NIN; ++i) in[i] = jobs[job].in[i];
         }
@@ -1068,8 +1105,8 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
   } else {
     // consumers: positions c, c + C, ... of the block's sequence
     const int c = wave - 2;
-    GfAcc<NOUT, ACC> body;
-    body.lds = lds;
+    typename Pol::Body body;
+    Pol::init(body, lds);
     g_cu4* in[NIN];
     int cur = -1;
     unsigned cur_lo = 0;  // first queue item of job `cur`
@@ -1114,8 +1151,7 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
         cur_lo = jn * RQ;
 #pragma unroll
         for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (jobs[jn].in[i]);
-#pragma unroll
-        for (int j = 0; j < NOUT; ++j) body.out[j] = (g_u4*) (jobs[jn].out[j]);
+        Pol::set_out(body, jobs + jn);
       }
       const unsigned job = static_cast<unsigned>(cur);
       const unsigned row = (u - cur_lo) * nq + q;
@@ -1138,21 +1174,15 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
       }
       // this job's tables: wait for them unless the loader has stopped
       bool tables = true;
-      if (ring_flag_ld(&tab_job) < job) {
+      if (Pol::kTables && ring_flag_ld(&tab_job) < job) {
         unsigned s4 = 0;
         while (ring_flag_ld(&tab_job) < job && ring_flag_ld(&bypass) == 0u && ++s4 < cap)
           __builtin_amdgcn_s_sleep(kRingSleep);
         tables = ring_flag_ld(&tab_job) >= job;
       }
       if (ok) {
-        if (tables) {
-          body.begin();
-          if (job & 1) body.template add<0, NIN, kTab>(x);
-          else body.template add<0, NIN, 0>(x);
-          body.finish(v);
-        } else {
-          gf_mac_vec_slow<NIN, NOUT, ACC>(jobs + job, in, v);
-        }
+        if (tables) Pol::combine(body, x, job, v);
+        else Pol::slow(jobs + job, in, v);
       }
       if (lane == 0) ring_flag_st(&prog[c], p + C);
     }
@@ -1172,7 +1202,7 @@ __device__ __forceinline__ void gf_mac_claimed(const GfLaunch& L) {
         for (unsigned i = 0; i < B; ++i) {
           const unsigned u = bb + i;
           const size_t v = vec_of(u);
-          if (row_ok(u) && v < nvec) gf_mac_vec_slow<NIN, NOUT, ACC>(jobs + job, jin, v);
+          if (row_ok(u) && v < nvec) Pol::slow(jobs + job, jin, v);
         }
       }
     }
@@ -1189,6 +1219,42 @@ __device__ __forceinline__ v4u* xor_lds() {
   __shared__ v4u ring[ring_vecs<NIN, R>()];
   return ring;
 }
+
+
+// XOR claimed launches (claimed_sweep): no tables; one-row positions in the
+// XOR kernels' own ring array (xor_lds, shared with xor_body: two-row items
+// of <= 8 inputs there, so twice the slots here)
+template <int NIN_, bool ACC>
+struct XorClaim {
+  static constexpr int NIN = NIN_;
+  static_assert(NIN <= kRingChunk, "claimed XOR of <= 8 inputs");
+  static constexpr int kRows = NIN > kRingXorWide ? 1 : kRingXorRows;  // xor_body's items
+  static constexpr bool kTables = false;
+  static constexpr int kSlots = ring_vecs<NIN, kRows>() / (NIN * 64);
+  static constexpr int kRingOff = 0;
+  using Launch = XorLaunch;
+  using Job = XorJob;
+  using Body = XorAcc<ACC>;
+  typedef __attribute__((address_space(4))) const XorJob c_job;
+  static __device__ __forceinline__ v4u* lds() { return xor_lds<NIN, kRows>(); }
+  static __device__ __forceinline__ void init(Body&, const uint32_t*) {}
+  static __device__ __forceinline__ void set_out(Body& b, const c_job* J) { b.out = (g_u4*) (J->out); }
+  static __device__ __forceinline__ void first_tables(uint32_t*, const c_job*, unsigned) {}
+  static __device__ __forceinline__ void next_tables(uint32_t*, const c_job*, unsigned, int) {}
+  static __device__ __forceinline__ void combine(Body& b, const v4u (&x)[NIN], unsigned, size_t v) {
+    b.begin();
+    b.template add<0>(x);
+    b.finish(v);
+  }
+  static __device__ __forceinline__ void slow(const c_job* J, g_cu4* const (&in)[NIN], size_t v) {
+    v4u r = ring_direct_load(in[0] + v);
+#pragma unroll
+    for (int i = 1; i < NIN; ++i) r ^= ring_direct_load(in[i] + v);
+    g_u4* o = (g_u4*) (J->out);
+    if constexpr (ACC) o[v] = r ^ o[v];
+    else store_vec(o, v, r);
+  }
+};
 
 template <int NIN, bool ACC>
 __device__ __forceinline__ void xor_stream(const XorLaunch& L) {
@@ -1371,7 +1437,7 @@ REDSET_KERNEL gf_mac_kernel(GfLaunch L) {
       return;
     }
     if (L.sequential == kJobsClaimed && L.claim && !L.bytes_only && L.nbytes % 16 == 0) {
-      gf_mac_claimed<NIN, NOUT, ACC>(L);
+      claimed_sweep<GfClaim<NIN, NOUT, ACC>>(L);
       return;
     }
   }
@@ -1398,6 +1464,10 @@ REDSET_KERNEL xor_kernel(XorLaunch L) {
   if constexpr (NIN <= kRingChunk) {
     if (L.sequential == kJobsStreamed && !L.bytes_only && L.nbytes % 16 == 0) {
       xor_stream<NIN, ACC>(L);
+      return;
+    }
+    if (L.sequential == kJobsClaimed && L.claim && !L.bytes_only && L.nbytes % 16 == 0) {
+      claimed_sweep<XorClaim<NIN, ACC>>(L);
       return;
     }
   }

@@ -35,7 +35,8 @@ constexpr int kJobsInKernel = 2;
 constexpr int kJobsStreamed = 3;
 // kJobsClaimed: as kJobsStreamed, but the blocks of each XCD claim their
 // items in batches from a shared per-XCD queue (GfLaunch::claim), so no block
-// runs ahead of the others or idles at the end (codec_device.h gf_mac_claimed).
+// runs ahead of the others or idles at the end (codec_device.h claimed_sweep;
+// GF and XOR jobs of <= 8 inputs over whole 16-B vectors).
 constexpr int kJobsClaimed = 4;
 // claim queues: one counter per XCD, 128 B apart (kClaimWords words per
 // launch, plan-owned; the launcher zeroes them on the launch's stream before
@@ -90,7 +91,9 @@ struct XorLaunch {
   int group;
   size_t nbytes;
   unsigned* fault;          // set by the launcher (see GfLaunch)
+  unsigned* claim;          // kJobsClaimed (see GfLaunch)
   unsigned spin_cap;        // (see GfLaunch)
+  unsigned claim_delay;     // (see GfLaunch)
 };
 
 // launchers (codec_kernels.hip); return hipError_t as int

@@ -196,6 +196,11 @@ int launch_xor(const XorLaunch& L, void* stream) {
     one.job0 = j;
     one.fault = ring_fault_word();
     one.spin_cap = spin_cap();
+    one.claim_delay = claim_delay();
+    if (L.sequential == kJobsClaimed && L.claim) {
+      const hipError_t e = hipMemsetAsync(L.claim, 0, kClaimWords * sizeof(unsigned), static_cast<hipStream_t>(stream));
+      if (e != hipSuccess) return e;
+    }
     if (L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) one.njobs = std::min(per, L.njobs - j);
     const int n = (L.sequential == kJobsInKernel || L.sequential == kJobsStreamed || L.sequential == kJobsClaimed)
                       ? 1

@@ -138,6 +138,10 @@ int stripes_per_launch(int order) {
 // REDSET_HIP_XOR_STREAM=1 streams them in pairs.
 bool xor_stream_default() { return test_knob("REDSET_HIP_XOR_STREAM", 0) == 1; }
 
+// XOR plans with claimed items (claimed_sweep, one launch per set): under
+// measurement, the twin's REDSET_HIP_XOR_CLAIM=1 (or REDSET_HIP_SEQUENTIAL=4)
+bool xor_claim_default() { return test_knob("REDSET_HIP_XOR_CLAIM", 0) == 1; }
+
 int launches_of(int order, int njobs, int group) {
   if (order == redset_hip::kJobsStreamed || order == redset_hip::kJobsClaimed)
     return group > 0 ? (njobs + group - 1) / group : 1;
@@ -278,7 +282,7 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     X.bytes_only = P.bytes_only;
     X.nbytes = nbytes;
     const bool whole = P.nin <= 8 && !P.bytes_only && nbytes % 16 == 0;
-    X.sequential = sequential_jobs(X.njobs, nbytes, whole, false, false, xor_stream_default());
+    X.sequential = sequential_jobs(X.njobs, nbytes, whole, whole, xor_claim_default(), xor_stream_default());
     X.group = stripes_per_launch(X.sequential);
     X.blocks_per_job = blocks_per_job(jobs_sharing_grid(X.sequential, X.njobs, X.group), nbytes, xor_blocks_cap());
     xall.insert(xall.end(), P.jobs.begin(), P.jobs.end());
@@ -300,6 +304,8 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
   size_t nclaim = 0;
   for (GfLaunch& G : plan->gf_launches)
     if (G.sequential == redset_hip::kJobsClaimed) ++nclaim;
+  for (XorLaunch& X : plan->xor_launches)
+    if (X.sequential == redset_hip::kJobsClaimed) ++nclaim;
   if (nclaim > 0) {
     const size_t bytes = nclaim * redset_hip::kClaimWords * sizeof(unsigned);
     if (int rc = hip_check(hipMalloc(&plan->d_claim, bytes), "hipMalloc(claim queues)")) return rc;
@@ -307,6 +313,8 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     size_t k = 0;
     for (GfLaunch& G : plan->gf_launches)
       if (G.sequential == redset_hip::kJobsClaimed) G.claim = plan->d_claim + (k++) * redset_hip::kClaimWords;
+    for (XorLaunch& X : plan->xor_launches)
+      if (X.sequential == redset_hip::kJobsClaimed) X.claim = plan->d_claim + (k++) * redset_hip::kClaimWords;
   }
   if (!xall.empty()) {
     if (int rc = hip_check(hipMalloc(&plan->d_xor, xall.size() * sizeof(XorJob)), "hipMalloc(plan jobs)")) return rc;

@@ -256,7 +256,7 @@ def test_xor_encode_and_rebuild(rd, oracle, p, chunk, padded):
 
 @pytest.mark.parametrize("mode,group,n_rs,n_xor", [("0", "1", 1, 1), ("1", "1", 11, 8), ("1", "3", 4, 3),
                                                    ("2", "1", 1, 1), ("3", "2", 6, 4), ("3", "0", 1, 1),
-                                                   ("3", "1", 11, 8), ("4", "0", 1, 8), ("4", "3", 4, 3)])
+                                                   ("3", "1", 11, 8), ("4", "0", 1, 1), ("4", "3", 4, 3)])
 @pytest.mark.knobs
 def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     """A plan runs its stripes side by side in one launch (REDSET_HIP_SEQUENTIAL=0),
@@ -265,7 +265,7 @@ def test_plan_job_order(rd, oracle, monkeypatch, mode, group, n_rs, n_xor):
     stripes in turn (=2), `group` stripes per launch streamed through one
     continuous ring (=3; REDSET_HIP_STREAM_JOBS, 0 = all) or the same with the
     items claimed at run time (=4, RS(8+3)'s default, all stripes in one
-    launch; XOR plans take =1 there): same bytes."""
+    launch, RS or XOR): same bytes."""
     monkeypatch.setenv("REDSET_HIP_SEQUENTIAL", mode)
     monkeypatch.setenv("REDSET_HIP_STRIPES_PER_LAUNCH", group)
     monkeypatch.setenv("REDSET_HIP_STREAM_JOBS", group)
@@ -374,6 +374,25 @@ def test_claimed_order_ragged_rows(rd, oracle, monkeypatch, chunk):
     gl, gp = download_set(lay)
     assert all(np.array_equal(a, b) for a, b in zip(gl, lofi))
     assert all(np.array_equal(a, b) for a, b in zip(gp, parity))
+    # XOR sets through the same claimed kernel (claimed_sweep without tables)
+    xl, xc = oracle.random_set(8, 7, 1, chunk, seed=chunk % 997)
+    xlay = upload_set(rd, xl, xc, 7, 1, chunk)
+    xenc = rd.xor_plan_encode(8, xlay.lofi_ptrs(), xlay.parity_ptrs(), chunk, xlay.cell_stride)
+    assert xenc.launches == 1
+    xenc.execute()
+    xenc.execute()
+    torch.cuda.synchronize()
+    oracle.xor_encode_set(8, xl, xc, chunk)
+    _, xgot = download_set(xlay)
+    assert all(np.array_equal(a, b) for a, b in zip(xgot, xc))
+    xlay.lofi(5).fill_(0x33)
+    xlay.parity(5).fill_(0x44)
+    xreb = rd.xor_plan_rebuild(8, 5, xlay.lofi_ptrs(), xlay.parity_ptrs(), chunk, xlay.cell_stride)
+    assert xreb.launches == 1
+    xreb.execute()
+    torch.cuda.synchronize()
+    gl, gp = download_set(xlay)
+    assert np.array_equal(gl[5], xl[5]) and np.array_equal(gp[5], xc[5])
 
 
 def test_claimed_encode_product_ragged_rows(rd, oracle):

@@ -103,3 +103,59 @@ def test_xor_sharded_plan_random(oracle, seed):
     res = run_group(cmd, 120, env=env, cwd="/tmp")
     assert res.returncode == 0, (np_, p, chunk, root, res.stdout + res.stderr)
     assert res.stdout.count("rebuild gather") == np_
+
+
+RANK_TEST = os.path.join(ROOT, "tests", "mpi", "build", "rank_test")
+
+
+def _rank_test_set(tmp, p, chunk):
+    for r in range(p):
+        path = os.path.join(tmp, f"r{r}.dat")
+        with open(path, "wb") as f:
+            f.write(bytes((r * 7 + i) & 0xFF for i in range(chunk * 2)))
+        with open(os.path.join(tmp, f"manifest_{r}.txt"), "w") as f:
+            f.write(f"1\n{path} {chunk * 2}\n{chunk}\n64\n{os.path.join(tmp, f'r{r}.red')}\n")
+        with open(os.path.join(tmp, f"r{r}.red"), "wb") as f:
+            f.write(b"H" * 64 + bytes(chunk * 2))
+
+
+@pytest.mark.parametrize("exchange,used", [("", "host"), ("host", "host"), ("sharded-mpi", "sharded-mpi")])
+def test_rebuild_exchange_choice_on_cpu(tmp_path, exchange, used):
+    """The per-rank decode's exchange choice (rank_mpi.c choose_exchange) is
+    collective and agreed before any exchange: on a machine without a GPU,
+    "auto" finds no GPU per member and takes the host path, a forced mode is
+    taken as asked, and the decode then fails on every member (no HIP device)
+    without a hang. The GPU tests run the same choices to completion."""
+    if not _have() or not os.path.exists(RANK_TEST):
+        pytest.skip("needs MPICH and tests/mpi/build/rank_test")
+    from conftest import gpu_available
+
+    if gpu_available():
+        pytest.skip("CPU-only check (on a GPU box the decode runs: tests/test_gpu_mpi.py)")
+    tmp = str(tmp_path)
+    _rank_test_set(tmp, 4, 1000)
+    env = {**os.environ}
+    env.pop("RANK_TEST_EXCHANGE", None)
+    if exchange:
+        env["RANK_TEST_EXCHANGE"] = exchange
+    cmd = [MPIRUN, "-np", "4", "-host", "localhost", RANK_TEST, "rs", "rebuild", "2", tmp, "4096", "1", "2"]
+    res = run_group(cmd, 60, env=env, cwd="/tmp")
+    assert res.returncode != 0
+    assert f"rebuild exchange {used}" in res.stdout, res.stdout + res.stderr
+    assert res.stderr.count("backend failed") == 4, res.stderr
+
+
+def test_rebuild_exchange_members_must_agree(tmp_path):
+    """Members asking for different exchanges fail together (one allreduce
+    of the mode) instead of deadlocking in mismatched exchanges."""
+    if not _have() or not os.path.exists(RANK_TEST):
+        pytest.skip("needs MPICH and tests/mpi/build/rank_test")
+    tmp = str(tmp_path)
+    _rank_test_set(tmp, 4, 1000)
+    args = [RANK_TEST, "rs", "rebuild", "2", tmp, "4096", "1", "2"]
+    cmd = [MPIRUN, "-host", "localhost", "-n", "1", "-env", "RANK_TEST_EXCHANGE", "sharded-mpi"] + args + \
+        [":", "-n", "3", "-env", "RANK_TEST_EXCHANGE", "host"] + args
+    res = run_group(cmd, 60, cwd="/tmp")
+    assert res.returncode != 0
+    assert "disagree on the rebuild exchange" in res.stderr, res.stderr
+    assert res.stderr.count("backend failed") == 4, res.stderr

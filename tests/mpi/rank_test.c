@@ -84,7 +84,7 @@ static void print_stats(int rank, const char* tag) {
   MPI_Reduce(v, sm, 11, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
   if (rank != 0) return;
   printf("rank_stats %s {", tag);
-  for (int i = 0; i < 11; ++i) printf("%s\"%s\": [%.6g, %.6g]", i ? ", " : "", names[i], mx[i], sm[i]);
+  for (int i = 0; i < 11; ++i) printf("%s\"%s\": [%.15g, %.15g]", i ? ", " : "", names[i], mx[i], sm[i]);
   printf("}\n");
 }
 
@@ -100,8 +100,16 @@ static void on_fatal(int sig) {
 
 int main(int argc, char** argv) {
   setvbuf(stdout, NULL, _IOLBF, 0);
-  signal(SIGSEGV, on_fatal);
-  signal(SIGBUS, on_fatal);
+  /* on its own stack, so a stack overflow is reported too */
+  static char alt[1 << 16];
+  stack_t ss = {.ss_sp = alt, .ss_size = sizeof(alt), .ss_flags = 0};
+  sigaltstack(&ss, NULL);
+  struct sigaction sa;
+  memset(&sa, 0, sizeof(sa));
+  sa.sa_handler = on_fatal;
+  sa.sa_flags = SA_ONSTACK;
+  sigaction(SIGSEGV, &sa, NULL);
+  sigaction(SIGBUS, &sa, NULL);
   MPI_Init(&argc, &argv);
   int rank, ranks;
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);

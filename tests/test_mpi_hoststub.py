@@ -1,0 +1,153 @@
+"""The per-rank backends' host code on the CPU (no GPU needed).
+
+libredset_hip_mpi.so's host-MPI path (redset_amd/csrc/rank_mpi.c: file reads,
+the ring exchange of redset's per-rank encode/rebuild, the scratch pool, the
+per-call stats, the writes) runs here with tests/mpi/hipstub.c preloaded in
+place of the HIP runtime and the two combine calls. The stub is test
+infrastructure only; the GPU suite (tests/test_gpu_mpi.py) runs the same
+driver, tests/mpi/rank_test.c, on the real runtime and kernels. A host-code
+regression (a self-recursive MPI wrapper once slipped through, because on a
+GPU-less machine the backends stop at hipStreamCreate) fails here first.
+
+Checks as in test_gpu_mpi.py: parity after each rank's header equals the
+oracle's on the padded logical files (test/test_redset.c:459-589), rebuilt
+files match by CRC32, and a member's I/O error fails every rank without a
+hang (src/redset_reedsolomon.c:338-342)."""
+import json
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from proc import run_group
+from test_gpu_mpi import _logical, _manifests, _setup
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+MPI_DIR = os.path.join(ROOT, "tests", "mpi")
+RANK_TEST = os.path.join(MPI_DIR, "build", "rank_test")
+STUB = os.path.join(MPI_DIR, "build", "libhipstub.so")
+MPIRUN = "/opt/conda/bin/mpirun"
+
+
+@pytest.fixture(scope="module")
+def stub():
+    if not os.path.exists(MPIRUN):
+        pytest.skip("needs MPICH")
+    if not os.path.exists(os.path.join(ROOT, "redset_amd", "lib", "libredset_hip_mpi.so")):
+        pytest.skip("libredset_hip_mpi.so not built")
+    subprocess.run(["make", "-s", "-C", MPI_DIR], check=True, capture_output=True)
+    return STUB
+
+
+def _run(np_, args, env=None, timeout=120):
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", "-env", "LD_PRELOAD", STUB, RANK_TEST] + \
+        [str(a) for a in args]
+    return run_group(cmd, timeout, env={**os.environ, **(env or {})})
+
+
+def _stats(stdout, tag="first"):
+    for line in stdout.splitlines():
+        if line.startswith(f"rank_stats {tag} "):
+            return json.loads(line.split(" ", 2)[2])
+    raise AssertionError(stdout)
+
+
+def _round_trip(oracle, tmp, scheme, p, e, lost, buf, seed, maxsize, header=None, env=None):
+    d = p - e
+    rng = np.random.default_rng(seed)
+    files, chunk = _setup(tmp, p, d, rng, maxsize)
+    header = header or [int(rng.integers(0, 5000)) for _ in range(p)]
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, header, reds)
+    crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
+    res = _run(p, [scheme, "encode", e, tmp, buf], env=env)
+    assert res.returncode == 0, res.stdout + res.stderr
+    lofi = [_logical(fl, d * chunk) for fl in files]
+    want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+    if scheme == "rs":
+        oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    else:
+        oracle.xor_encode_set(p, lofi, want, chunk)
+    for r in range(p):
+        blob = np.fromfile(reds[r], dtype=np.uint8)
+        assert blob.size == header[r] + e * chunk
+        assert np.array_equal(blob[header[r]:], want[r]), (scheme, p, e, r)
+    enc = res
+    for r in lost:
+        for path, _ in files[r]:
+            os.unlink(path)
+        os.unlink(reds[r])
+    res = _run(p, [scheme, "rebuild", e, tmp, buf] + lost, env=env)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "rebuild exchange host" in res.stdout, res.stdout
+    for r in lost:
+        for path, size in files[r]:
+            assert os.path.getsize(path) == size
+            assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
+        blob = np.fromfile(reds[r], dtype=np.uint8)
+        assert np.array_equal(blob[header[r]:header[r] + e * chunk], want[r]), r
+    return enc, res, chunk
+
+
+@pytest.mark.parametrize("scheme,p,e,lost,buf", [("rs", 6, 2, [1, 4], 65536), ("rs", 5, 3, [0, 2, 4], 40000),
+                                                  ("xor", 4, 1, [2], 50000), ("xor", 2, 1, [0], 4096),
+                                                  ("rs", 3, 1, [2], 100_003)])
+def test_host_path_round_trip(stub, oracle, tmp_path, scheme, p, e, lost, buf):
+    _round_trip(oracle, str(tmp_path), scheme, p, e, lost, buf, p * 10 + e, 200_000)
+
+
+@pytest.mark.parametrize("seed", range(6))
+def test_host_path_random(stub, oracle, tmp_path, seed):
+    rng = np.random.default_rng(4400 + seed)
+    scheme = "xor" if seed % 3 == 2 else "rs"
+    p = int(rng.integers(3 if scheme == "rs" else 2, 9))
+    e = 1 if scheme == "xor" else int(rng.integers(1, min(p - 1, 4) + 1))
+    buf = int(rng.choice([4096, 65536, 100_003]))
+    m = 1 if scheme == "xor" else int(rng.integers(1, e + 1))
+    lost = sorted(rng.choice(p, size=m, replace=False).tolist())
+    _round_trip(oracle, str(tmp_path), scheme, p, e, lost, buf, 5500 + seed, int(rng.choice([1000, 150_000])))
+
+
+@pytest.mark.parametrize("scheme,p,e,lost", [("rs", 6, 2, [1, 4]), ("xor", 5, 1, [3])])
+def test_host_path_repeated_calls_and_stats(stub, oracle, tmp_path, scheme, p, e, lost):
+    """Three calls per process on the cached scratch; the per-call stats
+    (include/redset_hip_mpi.h redset_hip_rank_last_stats) count the bytes the
+    call moved: every rank reads its d*chunk data bytes and writes its
+    e*chunk parity bytes on encode, and sends what its peers receive."""
+    enc, _, chunk = _round_trip(oracle, str(tmp_path), scheme, p, e, lost, 32768, 77 + p, 400_000,
+                                header=[256] * p, env={"RANK_TEST_REPEAT": "3"})
+    assert "call 3 of 3" in enc.stdout, enc.stdout
+    d = p - e
+    for tag in ("first", "warm"):
+        st = _stats(enc.stdout, tag)
+        assert st["read_bytes"] == [d * chunk, p * d * chunk], st
+        assert st["write_bytes"] == [e * chunk, p * e * chunk], st
+        assert st["sent_bytes"][1] == st["recv_bytes"][1] > 0, st
+        assert st["seconds"][0] >= st["mpi_seconds"][0] >= 0, st
+
+
+@pytest.mark.parametrize("scheme,op,fail", [("rs", "encode", 2), ("rs", "rebuild", 3), ("xor", "rebuild", 0),
+                                             ("xor", "encode", 1)])
+def test_host_path_read_failure_fails_every_rank(stub, oracle, tmp_path, scheme, op, fail):
+    tmp = str(tmp_path)
+    p, e = (4, 2) if scheme == "rs" else (4, 1)
+    rng = np.random.default_rng(3)
+    files, chunk = _setup(tmp, p, p - e, rng, 300_000)
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, [512] * p, reds)
+    buf = 16384
+    args = [scheme, "encode", e, tmp, buf]
+    if op == "rebuild":
+        res = _run(p, args)
+        assert res.returncode == 0, res.stdout + res.stderr
+        lost = [1] if scheme == "rs" else [2]
+        for r in lost:
+            for path, _ in files[r]:
+                os.unlink(path)
+            os.unlink(reds[r])
+        args = [scheme, "rebuild", e, tmp, buf] + lost
+    res = _run(p, args, env={"RANK_TEST_FAIL_READ": str(fail)}, timeout=90)
+    assert res.returncode != 0, res.stdout + res.stderr
+    assert "backend failed" in res.stderr, res.stderr
+    assert "signal" not in res.stderr, res.stderr

@@ -201,7 +201,7 @@ int main(int argc, char** argv) {
   CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
   const size_t ncell = (size_t) nstripe * (NIN + NOUT);
   unsigned char* base = nullptr;
-  CK(hipMalloc(&base, ncell * stride + 3 * cell));
+  CK(hipMalloc(&base, ncell * stride + NOUT * cell));  // + the reference copy of stripe 0's NOUT outputs
   CK(hipMemset(base, 0x5A, ncell * stride));
   // distinct input contents: byte pattern per cell, or (argv[2] = "rand")
   // uniform random bytes in every cell, as the codec bench uses

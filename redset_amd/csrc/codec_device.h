@@ -1223,7 +1223,9 @@ __device__ __forceinline__ v4u* xor_lds() {
 
 // XOR claimed launches (claimed_sweep): no tables; one-row positions in the
 // XOR kernels' own ring array (xor_lds, shared with xor_body: two-row items
-// of <= 8 inputs there, so twice the slots here)
+// of <= 8 inputs there, so twice the slots here). A twin-only order: it
+// measured 8% slower than a launch per stripe (redset_hip.cpp
+// xor_claim_default)
 template <int NIN_, bool ACC>
 struct XorClaim {
   static constexpr int NIN = NIN_;

@@ -138,8 +138,13 @@ int stripes_per_launch(int order) {
 // REDSET_HIP_XOR_STREAM=1 streams them in pairs.
 bool xor_stream_default() { return test_knob("REDSET_HIP_XOR_STREAM", 0) == 1; }
 
-// XOR plans with claimed items (claimed_sweep, one launch per set): under
-// measurement, the twin's REDSET_HIP_XOR_CLAIM=1 (or REDSET_HIP_SEQUENTIAL=4)
+// XOR plans with claimed items (claimed_sweep, one launch per set): a measured
+// negative, kept as a twin-only order (REDSET_HIP_XOR_CLAIM=1 or
+// REDSET_HIP_SEQUENTIAL=4) the suite checks bit for bit: the XOR leg 5.60
+// against 5.98-6.09 TB/s. Its one-row items and claim bookkeeping cost +27%
+// SALU, +44% VALU and +54% LDS instructions per byte at equal HBM traffic,
+// and with consumers this light the loader's per-item instruction stream sets
+// the pace (profiles/r04s5_ab_xor_claim.txt, r04s6_xor_claim_pmc_sq.txt)
 bool xor_claim_default() { return test_knob("REDSET_HIP_XOR_CLAIM", 0) == 1; }
 
 int launches_of(int order, int njobs, int group) {

@@ -28,7 +28,46 @@
 
 #define DEFAULT_BUF ((size_t) 1 << 20) /* redset_mpi_buf_size default, src/redset.c:45 */
 #define MAX_SCRATCH 12
-#define MAX_STAGE ((size_t) 32 << 20) /* RS encode: bytes of ring slices staged per window (x2 buffers) */
+#define MAX_STAGE ((size_t) 96 << 20) /* RS encode: bytes of ring slices staged per window (x2 buffers) */
+/* REDSET_HIP_TEST_KNOBS=1: the test twin build (redset_amd/lib_test), whose
+ * backends honour the suite's injection and A/B variables; the product reads
+ * none */
+#ifndef REDSET_HIP_TEST_KNOBS
+#define REDSET_HIP_TEST_KNOBS 0
+#endif
+
+/* Bytes each step of a host-MPI exchange moves per cell: the slice. The
+ * reference moves redset_mpi_buf_size B per message (src/redset.c:45,
+ * default 1 MiB). Here B is raised to SLICE_MIN: on one box's shared-memory
+ * MPI, 4 MiB slices rebuild RS(8+3) 64 MiB chunks in 0.34 s against 0.62 s
+ * at 1 MiB and 0.63 s at 16 MiB, and encode (whole ring windows) in 0.69 s
+ * against 0.94 / 0.83 s (profiles/r04s7_rank_slice.txt). Two caps keep it
+ * from growing past what pays: at least SLICES_MIN slices per chunk, so the
+ * exchange of slice n still overlaps slice n-1's GPU work and writes (a 16
+ * MiB buffer over a 64 MiB chunk leaves 4, too few to pipeline), and at most
+ * SLICE_BUDGET of page-locked slice buffers per call (`cells` = the
+ * slice-sized host buffers the backend holds); a cut never goes below B or 1
+ * MiB, whichever is smaller (small chunks keep the caller's B). Every member
+ * derives the same slice from the same arguments. */
+#define SLICE_MIN ((size_t) 4 << 20)
+#define SLICES_MIN 16
+#define SLICE_BUDGET ((size_t) 256 << 20)
+static size_t slice_bytes(size_t B, size_t chunk_size, size_t cells) {
+#if REDSET_HIP_TEST_KNOBS
+  /* test builds: REDSET_HIP_TEST_RANK_SLICE=raw moves B per step (A/B runs) */
+  const char* v = getenv("REDSET_HIP_TEST_RANK_SLICE");
+  if (v && strcmp(v, "raw") == 0) return B;
+#endif
+  const size_t mib = (size_t) 1 << 20;
+  const size_t floor = B < mib ? B : mib; /* a cut never goes below this */
+  size_t s = B > SLICE_MIN ? B : SLICE_MIN;
+  size_t per = (chunk_size + SLICES_MIN - 1) / SLICES_MIN;
+  per = (per + 4095) / 4096 * 4096;
+  size_t fit = SLICE_BUDGET / (cells ? cells : 1) / 4096 * 4096;
+  if (s > per) s = per;
+  if (s > fit) s = fit;
+  return s > floor ? s : floor;
+}
 
 static int fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));
 static int fail(const char* fmt, ...) {
@@ -315,9 +354,6 @@ static int agree_setup(MPI_Comm comm, int rc) {
  * first device step report a failure (tests/mpi/rank_test.c drives it), so
  * the keep-the-collective-going path below is exercised without a broken
  * GPU. The product library reads no such variable. */
-#ifndef REDSET_HIP_TEST_KNOBS
-#define REDSET_HIP_TEST_KNOBS 0
-#endif
 static int injected_device_failure(MPI_Comm comm) {
   if (!REDSET_HIP_TEST_KNOBS) return 0;
   static int fired = 0;
@@ -370,13 +406,19 @@ static int rs_encode_impl(const redset_hip_rs* rs, MPI_Comm comm, const redset_h
    * peers would wait for it in the first collective */
   const int hrc = header_size(fd_chunk, chunk_file, &header);
   const int d = p - e;
-  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
-  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
+  const size_t buf = buf_size ? buf_size : DEFAULT_BUF;
+  if (buf > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", buf); /* same on every rank */
+  const size_t B = slice_bytes(buf, chunk_size, (size_t) 3 * e);
   /* ring steps staged per window: the d*e slices of a slice's whole ring
    * would need d*e*B of pinned and device memory (O(p*e)); windows of G steps
    * bound each staging buffer to MAX_STAGE, the reference's own scratch being
    * e+e+1 slices */
-  int G = (int) (MAX_STAGE / ((size_t) e * B));
+  size_t stage = MAX_STAGE;
+#if REDSET_HIP_TEST_KNOBS
+  /* test builds: the staging bound, for A/B runs (tools/rank_bench.py) */
+  if (getenv("REDSET_HIP_TEST_RANK_STAGE_MIB")) stage = (size_t) atoll(getenv("REDSET_HIP_TEST_RANK_STAGE_MIB")) << 20;
+#endif
+  int G = (int) (stage / ((size_t) e * B));
   if (G < 1) G = 1;
   if (G > d) G = d;
 
@@ -710,8 +752,9 @@ static int xor_encode_impl(MPI_Comm comm, const redset_hip_io* lofi, const char*
   /* a bad fd on one member is agreed on below, not returned early: its
    * peers would wait for it in the first collective */
   const int hrc = header_size(fd_chunk, chunk_file, &header);
-  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
-  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
+  const size_t buf = buf_size ? buf_size : DEFAULT_BUF;
+  if (buf > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", buf); /* same on every rank */
+  const size_t B = slice_bytes(buf, chunk_size, (size_t) 3 * p + 2);
 
   const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
   MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) p);
@@ -1225,7 +1268,7 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   g_last_exchange = mode;
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
                ? rs_decode_host(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
-                                header, hrc, chunk_size, B)
+                                header, hrc, chunk_size, slice_bytes(B, chunk_size, (size_t) (4 * p + 2 * missing)))
                : decode_sharded(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
                                 header, hrc, chunk_size, B, &tr);
   redset_hip_mpi_transport_destroy(mt);
@@ -1255,7 +1298,8 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   }
   g_last_exchange = mode;
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
-               ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B)
+               ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size,
+                                 slice_bytes(B, chunk_size, (size_t) 2 * p + 2))
                : decode_sharded(NULL, comm, p, r, 1, 1, &root, r == root, lofi, chunk_file, fd_chunk, header, hrc,
                                 chunk_size, B, &tr);
   redset_hip_mpi_transport_destroy(mt);

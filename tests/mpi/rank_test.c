@@ -207,7 +207,7 @@ int main(int argc, char** argv) {
     fsync(fd);
     double d = MPI_Wtime() - ti, dm = 0;
     MPI_Reduce(&d, &dm, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
-    if (rank == 0 && it == repeat - 1) printf("rank_test: call %d of %d (warm): %.4f s\n", it + 1, repeat, dm);
+    if (rank == 0) printf("rank_test: call %d of %d%s: %.4f s\n", it + 1, repeat, it == repeat - 1 ? " (warm)" : "", dm);
     if (it == repeat - 1) print_stats(rank, "warm");
   }
   close(fd);

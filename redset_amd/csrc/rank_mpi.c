@@ -36,12 +36,16 @@
 #define REDSET_HIP_TEST_KNOBS 0
 #endif
 
-/* Bytes each step of a host-MPI exchange moves per cell: the slice. The
+/* Bytes each step of the RS host-MPI exchange moves per cell: the slice. The
  * reference moves redset_mpi_buf_size B per message (src/redset.c:45,
  * default 1 MiB). Here B is raised to SLICE_MIN: on one box's shared-memory
- * MPI, 4 MiB slices rebuild RS(8+3) 64 MiB chunks in 0.34 s against 0.62 s
- * at 1 MiB and 0.63 s at 16 MiB, and encode (whole ring windows) in 0.69 s
- * against 0.94 / 0.83 s (profiles/r04s7_rank_slice.txt). Two caps keep it
+ * MPI, RS(8+3) over 11 ranks with 64 MiB chunks and a 1 MiB buffer rebuilds
+ * in 0.34-0.41 s against 0.61-0.62 s, and encodes (whole ring windows) in
+ * 0.78-0.86 s against 1.02-1.07 s; 16 MiB chunks with a 16 MiB buffer (cut
+ * to 1 MiB slices) 0.19 against 0.35 s and 0.23-0.26 against 0.31-0.32 s
+ * (median of 6 warm calls, two alternating runs each,
+ * profiles/r04s9_rank_slice.txt). The XOR backends keep B: larger slices
+ * measured slower there. Two caps keep it
  * from growing past what pays: at least SLICES_MIN slices per chunk, so the
  * exchange of slice n still overlaps slice n-1's GPU work and writes (a 16
  * MiB buffer over a 64 MiB chunk leaves 4, too few to pipeline), and at most
@@ -752,9 +756,10 @@ static int xor_encode_impl(MPI_Comm comm, const redset_hip_io* lofi, const char*
   /* a bad fd on one member is agreed on below, not returned early: its
    * peers would wait for it in the first collective */
   const int hrc = header_size(fd_chunk, chunk_file, &header);
-  const size_t buf = buf_size ? buf_size : DEFAULT_BUF;
-  if (buf > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", buf); /* same on every rank */
-  const size_t B = slice_bytes(buf, chunk_size, (size_t) 3 * p + 2);
+  /* the caller's buffer as the slice: the RS rule (slice_bytes) measured
+   * slower here (r04s9: 0.24-0.26 s against 0.17-0.23 s, XOR p = 8, 64 MiB) */
+  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
 
   const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
   MPI_Request* req = malloc(sizeof(*req) * 2 * (size_t) p);
@@ -1298,8 +1303,7 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   }
   g_last_exchange = mode;
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
-               ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size,
-                                 slice_bytes(B, chunk_size, (size_t) 2 * p + 2))
+               ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B)
                : decode_sharded(NULL, comm, p, r, 1, 1, &root, r == root, lofi, chunk_file, fd_chunk, header, hrc,
                                 chunk_size, B, &tr);
   redset_hip_mpi_transport_destroy(mt);

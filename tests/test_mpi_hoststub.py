@@ -155,8 +155,9 @@ def test_host_path_read_failure_fails_every_rank(stub, oracle, tmp_path, scheme,
 
 @pytest.mark.parametrize("scheme,p,e,lost", [("rs", 5, 2, [0, 3]), ("xor", 4, 1, [1])])
 def test_host_path_slices_larger_than_buffer(stub, oracle, tmp_path, scheme, p, e, lost):
-    """Chunks of ~20 MB with a 64 KiB buffer: the backends move slices of
+    """Chunks of ~20 MB with a 64 KiB buffer: the RS backends move slices of
     chunk/16 (~1.3 MB, rank_mpi.c slice_bytes), not the caller's buffer, and
-    the RS encode stages whole ring windows; parity and rebuilt files must not
-    depend on the slice."""
+    the RS encode stages whole ring windows (XOR keeps the buffer: the same
+    shapes as a control); parity and rebuilt files must not depend on the
+    slice."""
     _round_trip(oracle, str(tmp_path), scheme, p, e, lost, 65536, 31 + p, 20_000_000)

@@ -37,9 +37,9 @@ for probe in "$@"; do
     rank)
       for ex in host sharded-mpi; do
         run rank_rs_64m_$ex 400 python tools/rank_bench.py --ranks 11 --encoding 3 --chunk-mib 64 --buf-mib 16 \
-          --repeat 3 --exchange $ex --dir /tmp/rank_bench_$ex
+          --repeat 5 --exchange $ex --dir /tmp/rank_bench_$ex
         run rank_config0_$ex 200 python tools/rank_bench.py --scheme xor --ranks 4 --file-bytes 16777216 \
-          --buf-mib 1 --repeat 3 --exchange $ex --lost 2 --dir /tmp/rank_c0_$ex
+          --buf-mib 1 --repeat 5 --exchange $ex --lost 2 --dir /tmp/rank_c0_$ex
       done ;;
     wide)
       W="--ranks 20 --encoding 4 --lost 1,2,3,4 --cpu-baseline 0 --pairs 0 --xor 0"

@@ -63,14 +63,14 @@ static size_t slice_bytes(size_t B, size_t chunk_size, size_t cells) {
   if (v && strcmp(v, "raw") == 0) return B;
 #endif
   const size_t mib = (size_t) 1 << 20;
-  const size_t floor = B < mib ? B : mib; /* a cut never goes below this */
+  const size_t least = B < mib ? B : mib; /* a cut never goes below this */
   size_t s = B > SLICE_MIN ? B : SLICE_MIN;
   size_t per = (chunk_size + SLICES_MIN - 1) / SLICES_MIN;
   per = (per + 4095) / 4096 * 4096;
   size_t fit = SLICE_BUDGET / (cells ? cells : 1) / 4096 * 4096;
   if (s > per) s = per;
   if (s > fit) s = fit;
-  return s > floor ? s : floor;
+  return s > least ? s : least;
 }
 
 static int fail(const char* fmt, ...) __attribute__((format(printf, 1, 2)));

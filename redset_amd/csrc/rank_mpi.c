@@ -1116,6 +1116,10 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
   const int d = p - e, ncell = p, world = p;
   const int xor_scheme = rs == NULL;
   size_t win = SHARDED_WINDOW / (size_t) ncell;
+#if REDSET_HIP_TEST_KNOBS
+  /* test builds: small windows, so small sets take several (the mid-call stop) */
+  if (getenv("REDSET_HIP_TEST_SHARDED_WINDOW")) win = (size_t) atoll(getenv("REDSET_HIP_TEST_SHARDED_WINDOW"));
+#endif
   if (win < B) win = B;
   if (win > chunk_size) win = chunk_size;
   if (win == 0) win = 1;
@@ -1190,6 +1194,7 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
         break;
       }
       hipStream_t s = S.stream;
+      if (!rc) rc = injected_device_failure(comm);
       for (int x = 0; x < ncell && !rc; ++x) {
         if (!want[x]) continue;
         uint8_t* dst = x < d ? hd[b] + (size_t) x * W : hp[b] + (size_t) (x - d) * W;
@@ -1199,7 +1204,10 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
           rc = fail("H2D copy failed");
         g_stats.h2d_bytes += WW;
       }
-      if (!rc && redset_hip_sharded_execute(*P, s) != 0) rc = REDSET_FAILURE;
+      /* the exchange runs whatever this member's state since the agreement:
+       * its peers are in it (a member whose copies failed sends what its
+       * buffers hold, and every member stops at the next window's agreement) */
+      if (redset_hip_sharded_execute(*P, s) != 0 && !rc) rc = REDSET_FAILURE;
       redset_hip_sharded_info info;
       if (!rc && redset_hip_sharded_get_info(*P, &info) == 0) {
         g_stats.sent_bytes += info.gather_bytes_sent + info.return_bytes_sent;
@@ -1318,37 +1326,46 @@ struct redset_hip_mpi_transport {
   MPI_Comm comm;
   int world, rank, device;
   int hip_host;     /* host buffers that HIP kernels on `stream` read and write */
-  uint8_t* stage;   /* pinned staging (device mode) */
+  uint8_t* stage;   /* staging (device mode): pinned, or malloc'd if pinning failed */
   size_t stage_len;
+  int stage_pinned;
   MPI_Request* req;
   int req_cap;
 };
 
+/* Every message of the exchange is posted and waited for even after a HIP
+ * error on this member (its peers are in the same exchange and would hang,
+ * src/redset_reedsolomon.c:338-342): the error is returned at the end, and
+ * the bytes this member sent are unspecified. */
 static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream) {
   struct redset_hip_mpi_transport* T = (struct redset_hip_mpi_transport*) ctx;
   hipStream_t s = (hipStream_t) stream;
+  int rc = 0;
   size_t need = 0, nreq = 0;
   for (int i = 0; i < n; ++i)
     if (x[i].peer != T->rank) {
       need += x[i].len;
       nreq += (x[i].len + MPI_PIECE - 1) / MPI_PIECE;
     }
-  if (T->device) {
-    if (need > T->stage_len) {
-      if (T->stage) (void) hipHostFree(T->stage);
-      T->stage = NULL;
-      T->stage_len = 0;
-      if (hipHostMalloc((void**) &T->stage, need, hipHostMallocDefault) != hipSuccess)
-        return fail("mpi transport: hipHostMalloc(%zu) failed", need);
-      T->stage_len = need;
+  if (T->device && need > T->stage_len) {
+    if (T->stage) T->stage_pinned ? (void) hipHostFree(T->stage) : free(T->stage);
+    T->stage = NULL;
+    T->stage_len = 0;
+    T->stage_pinned = hipHostMalloc((void**) &T->stage, need, hipHostMallocDefault) == hipSuccess;
+    if (!T->stage_pinned) {
+      /* pageable memory still carries the messages */
+      T->stage = malloc(need);
+      rc = fail("mpi transport: hipHostMalloc(%zu) failed", need);
     }
+    if (!T->stage) return fail("mpi transport: out of host memory (%zu)", need);
+    T->stage_len = need;
   }
   /* work already on the stream produced the send buffers -- in host mode
    * too, where a HIP compute over page-locked slabs may still be writing
    * them, on the null stream as well (device_buffers = 2); a host-only
    * caller (device_buffers = 0, no stream) needs no HIP runtime */
   if ((T->device || T->hip_host || s) && hipStreamSynchronize(s) != hipSuccess)
-    return fail("mpi transport: stream sync failed");
+    rc = fail("mpi transport: stream sync failed");
   if ((int) nreq > T->req_cap) {
     MPI_Request* r = realloc(T->req, sizeof(*r) * nreq);
     if (!r) return fail("out of host memory");
@@ -1360,22 +1377,22 @@ static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream
   for (int i = 0; i < n; ++i) {
     if (x[i].peer == T->rank) {
       if (i + 1 >= n || !x[i].send || x[i + 1].send || x[i + 1].peer != T->rank || x[i + 1].len != x[i].len)
-        return fail("mpi transport: malformed local copy");
-      if (T->device) {
+        return fail("mpi transport: malformed local copy"); /* a plan bug, the same on every member */
+      if (!rc && T->device) {
         if (hipMemcpyAsync(x[i + 1].buf, x[i].buf, x[i].len, hipMemcpyDeviceToDevice, s) != hipSuccess)
-          return fail("mpi transport: local copy failed");
-      } else {
+          rc = fail("mpi transport: local copy failed");
+      } else if (!rc) {
         memmove(x[i + 1].buf, x[i].buf, x[i].len);
       }
       ++i;
       continue;
     }
-    if (T->device && x[i].send &&
+    if (!rc && T->device && x[i].send &&
         hipMemcpyAsync(T->stage + off, x[i].buf, x[i].len, hipMemcpyDeviceToHost, s) != hipSuccess)
-      return fail("mpi transport: D2H staging failed");
+      rc = fail("mpi transport: D2H staging failed");
     off += x[i].len;
   }
-  if (T->device && hipStreamSynchronize(s) != hipSuccess) return fail("mpi transport: stream sync failed");
+  if (!rc && T->device && hipStreamSynchronize(s) != hipSuccess) rc = fail("mpi transport: stream sync failed");
   int k = 0;
   off = 0;
   for (int i = 0; i < n; ++i) {
@@ -1392,7 +1409,7 @@ static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream
     off += x[i].len;
   }
   if (MPI_Waitall(k, T->req, MPI_STATUSES_IGNORE) != MPI_SUCCESS) return fail("mpi transport: MPI_Waitall failed");
-  if (!T->device) return 0;
+  if (!T->device || rc) return rc;
   off = 0;
   for (int i = 0; i < n; ++i) {
     if (x[i].peer == T->rank) {
@@ -1434,7 +1451,8 @@ int redset_hip_mpi_transport_create(MPI_Comm comm, int device_buffers, redset_hi
 
 void redset_hip_mpi_transport_destroy(redset_hip_mpi_transport* T) {
   if (!T) return;
-  if (T->stage) (void) hipHostFree(T->stage);
+  if (T->stage && T->stage_pinned) (void) hipHostFree(T->stage);
+  else free(T->stage);
   free(T->req);
   free(T);
 }

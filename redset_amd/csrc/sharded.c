@@ -520,46 +520,56 @@ static int hfail(const char* what, hipError_t e) { return sfail("sharded execute
  * R(n-1); caller's stream: C0 .. C(n-1), each after its gather. Both start
  * after the work already on `stream`, and `stream` resumes after the last
  * return. A transport that completes its exchange before returning (MPI)
- * overlaps the same way: the host runs gather k+1 while the GPU computes k. */
+ * overlaps the same way: the host runs gather k+1 while the GPU computes k.
+ * After a local HIP or compute error every exchange still runs (the other
+ * members are in them and would wait forever, src/redset_reedsolomon.c:
+ * 338-342): the bytes this member sends are then unspecified, and the error
+ * is returned at the end. */
 static int execute_pipelined(redset_hip_sharded* P, hipStream_t s) {
   hipError_t e;
+  int rc = 0;
   const int n = P->info.nsets;
-  if (!P->xstream) {
+  if (!P->xstream && !P->ev_c) {
     P->ev_c = calloc((size_t) n, sizeof(hipEvent_t));
-    if (!P->ev_c) return sfail("out of host memory");
-    if ((e = hipStreamCreateWithFlags(&P->xstream, hipStreamNonBlocking)) != hipSuccess) return hfail("stream", e);
-    if ((e = hipEventCreateWithFlags(&P->ev_x, hipEventDisableTiming)) != hipSuccess) return hfail("event", e);
-    for (int k = 0; k < n; ++k)
-      if ((e = hipEventCreateWithFlags(&P->ev_c[k], hipEventDisableTiming)) != hipSuccess) return hfail("event", e);
+    if (!P->ev_c) rc = sfail("out of host memory");
+    if (!rc && (e = hipStreamCreateWithFlags(&P->xstream, hipStreamNonBlocking)) != hipSuccess) rc = hfail("stream", e);
+    if (!rc && (e = hipEventCreateWithFlags(&P->ev_x, hipEventDisableTiming)) != hipSuccess) rc = hfail("event", e);
+    for (int k = 0; k < n && !rc; ++k)
+      if ((e = hipEventCreateWithFlags(&P->ev_c[k], hipEventDisableTiming)) != hipSuccess) rc = hfail("event", e);
+  } else if (!P->xstream || !P->ev_x) {
+    rc = sfail("sharded execute: the plan's stream or events were not created");
   }
-  hipStream_t x = P->xstream;
+  /* without its own stream (a failed setup) the exchanges go on `s` */
+  hipStream_t x = P->xstream ? P->xstream : s;
   /* the exchange stream starts after the caller's work (ev_c[0] is free until
    * compute 0 records it) */
-  if ((e = hipEventRecord(P->ev_c[0], s)) != hipSuccess || (e = hipStreamWaitEvent(x, P->ev_c[0], 0)) != hipSuccess)
-    return hfail("order after the caller's stream", e);
+  if (!rc && ((e = hipEventRecord(P->ev_c[0], s)) != hipSuccess || (e = hipStreamWaitEvent(x, P->ev_c[0], 0)) != hipSuccess))
+    rc = hfail("order after the caller's stream", e);
   for (int k = 0; k < n; ++k) {
-    if (exchange(P, &P->gather, P->goff[k], P->goff[k + 1], x, "gather")) return REDSET_FAILURE;
-    if ((e = hipEventRecord(P->ev_x, x)) != hipSuccess || (e = hipStreamWaitEvent(s, P->ev_x, 0)) != hipSuccess)
-      return hfail("gather -> compute", e);
-    if (compute_set(P, k, s)) return REDSET_FAILURE;
-    if ((e = hipEventRecord(P->ev_c[k], s)) != hipSuccess) return hfail("compute event", e);
+    if (exchange(P, &P->gather, P->goff[k], P->goff[k + 1], x, "gather") && !rc) rc = REDSET_FAILURE;
+    if (!rc && ((e = hipEventRecord(P->ev_x, x)) != hipSuccess || (e = hipStreamWaitEvent(s, P->ev_x, 0)) != hipSuccess))
+      rc = hfail("gather -> compute", e);
+    if (!rc && compute_set(P, k, s)) rc = REDSET_FAILURE;
+    if (!rc && (e = hipEventRecord(P->ev_c[k], s)) != hipSuccess) rc = hfail("compute event", e);
   }
   for (int k = 0; k < n; ++k) {
     if (P->roff[k + 1] == P->roff[k]) continue;
-    if ((e = hipStreamWaitEvent(x, P->ev_c[k], 0)) != hipSuccess) return hfail("compute -> return", e);
-    if (exchange(P, &P->ret, P->roff[k], P->roff[k + 1], x, "return")) return REDSET_FAILURE;
+    if (!rc && (e = hipStreamWaitEvent(x, P->ev_c[k], 0)) != hipSuccess) rc = hfail("compute -> return", e);
+    if (exchange(P, &P->ret, P->roff[k], P->roff[k + 1], x, "return") && !rc) rc = REDSET_FAILURE;
   }
-  if ((e = hipEventRecord(P->ev_x, x)) != hipSuccess || (e = hipStreamWaitEvent(s, P->ev_x, 0)) != hipSuccess)
-    return hfail("order the caller's stream after the returns", e);
-  return REDSET_SUCCESS;
+  if (!rc && ((e = hipEventRecord(P->ev_x, x)) != hipSuccess || (e = hipStreamWaitEvent(s, P->ev_x, 0)) != hipSuccess))
+    rc = hfail("order the caller's stream after the returns", e);
+  return rc;
 }
 
 int redset_hip_sharded_execute(redset_hip_sharded* P, void* stream) {
   if (!P) return sfail("null sharded plan");
   if (P->comp.run) {
+    /* every phase runs after a failed one (see execute_pipelined) */
+    int rc = 0;
     for (int ph = REDSET_HIP_PHASE_GATHER; ph <= REDSET_HIP_PHASE_RETURN; ++ph)
-      if (redset_hip_sharded_execute_phase(P, ph, stream)) return REDSET_FAILURE;
-    return REDSET_SUCCESS;
+      if (redset_hip_sharded_execute_phase(P, ph, stream) && !rc) rc = REDSET_FAILURE;
+    return rc;
   }
   return execute_pipelined(P, (hipStream_t) stream);
 }

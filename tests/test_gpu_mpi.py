@@ -46,15 +46,22 @@ def _mpirun(np_, args, timeout=300, env=None):
 # the members share one GPU, so auto must take the host path --, and
 # "sharded-mpi" runs the same sharded plan (gather column slices, gf_mac on
 # every GPU, return) over the MPI transport with device buffers
-EXCHANGES = ["auto", "sharded-mpi"]
+EXCHANGES = ["auto", "sharded-mpi", "sharded-mpi-windows"]
+TWIN_DIR = os.path.join(ROOT, "redset_amd", "lib_test")
 
 
 def _exchange_env(exchange):
+    if exchange == "sharded-mpi-windows":
+        # the test twin (loaded ahead of the driver's RUNPATH) with 64 KiB
+        # windows: small sets take several windows, double-buffered
+        ld = os.environ.get("LD_LIBRARY_PATH")
+        return {"RANK_TEST_EXCHANGE": "sharded-mpi", "REDSET_HIP_TEST_SHARDED_WINDOW": "65536",
+                "LD_LIBRARY_PATH": TWIN_DIR + (":" + ld if ld else "")}
     return {"RANK_TEST_EXCHANGE": exchange}
 
 
 def _check_exchange(res, exchange):
-    used = "host" if exchange == "auto" else exchange
+    used = "host" if exchange == "auto" else exchange.replace("-windows", "")
     assert f"rebuild exchange {used}" in res.stdout, res.stdout
 
 
@@ -146,6 +153,14 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf, exchange):
     ("rs", "rebuild", {"RANK_TEST_FAIL_READ": "3", "RANK_TEST_EXCHANGE": "sharded-mpi"}),
     ("rs", "rebuild", {"RANK_TEST_FAIL_READ": "0", "RANK_TEST_EXCHANGE": "sharded-mpi"}),
     ("xor", "rebuild", {"RANK_TEST_FAIL_READ": "1", "RANK_TEST_EXCHANGE": "sharded-mpi"}),
+    # a device error after the window's agreement: the failing member still
+    # runs the window's exchange (its peers are in it) and every member stops
+    # at the next agreement (test twin: 64 KiB windows, several per call)
+    ("rs", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2", "RANK_TEST_EXCHANGE": "sharded-mpi",
+                       "REDSET_HIP_TEST_SHARDED_WINDOW": "65536"}),
+    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "3", "RANK_TEST_EXCHANGE": "sharded-mpi",
+                        "REDSET_HIP_TEST_SHARDED_WINDOW": "65536"}),
+    ("rs", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "0", "RANK_TEST_EXCHANGE": "sharded-mpi"}),
 ])
 def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme, op, env):
     """One member's I/O or device error in the middle of the loop: that member
@@ -176,7 +191,7 @@ def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme
         args = [scheme, "encode", e, tmp, buf]
     cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST] + [str(a) for a in args]
     env = {**os.environ, **env}
-    if "REDSET_HIP_INJECT_DEVICE_FAILURE" in env:
+    if any(k == "REDSET_HIP_INJECT_DEVICE_FAILURE" or k.startswith("REDSET_HIP_TEST_") for k in env):
         # only the test twin honours the injection knob (the product reads no
         # environment): the driver loads it ahead of its RUNPATH
         twin = os.path.join(ROOT, "redset_amd", "lib_test")
@@ -349,7 +364,7 @@ def test_mpi_rank_backends_random(oracle, tmp_path, seed):
         for path, _ in files[r]:
             os.unlink(path)
         os.unlink(reds[r])
-    exchange = EXCHANGES[seed % 2]
+    exchange = EXCHANGES[seed % 3]
     res = _mpirun(p, [scheme, "rebuild", e, tmp, buf] + lost, timeout=120, env=_exchange_env(exchange))
     assert res.returncode == 0, (scheme, p, e, buf, lost, exchange, res.stdout + res.stderr)
     _check_exchange(res, exchange)

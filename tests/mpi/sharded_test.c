@@ -42,6 +42,9 @@
 
 static int P, E, D, XOR;
 static ro_rs* ORACLE;
+/* SHARDED_TEST_FAIL_COMPUTE=<rank>: that process's compute callback fails in
+ * the encode (the plan must still run every exchange, or its peers hang) */
+static int ME, FAIL_COMPUTE = -1;
 
 static uint8_t byte_of(int k, int r, size_t i) { /* member (k, r)'s logical-file byte i */
   uint64_t z = ((uint64_t) k << 48) ^ ((uint64_t) r << 32) ^ (uint64_t) i ^ 0x5EEDULL;
@@ -70,6 +73,7 @@ static int fill_slab(void* dst, int v, size_t n) {
 /* compute callback: the oracle on compacted copies of the slices */
 static int oracle_run(void* ctx, int kind, int missing, const int* lost, unsigned char* const* lofi,
                       unsigned char* const* parity, size_t n, size_t W, void* stream) {
+  if (ME == FAIL_COMPUTE && (kind == REDSET_HIP_PLAN_RS_ENCODE || kind == REDSET_HIP_PLAN_XOR_ENCODE)) return 1;
   uint8_t** lf = malloc(sizeof(*lf) * P);
   uint8_t** pr = malloc(sizeof(*pr) * P);
   for (int r = 0; r < P; ++r) {
@@ -100,6 +104,8 @@ int main(int argc, char** argv) {
   int world, me;
   MPI_Comm_size(MPI_COMM_WORLD, &world);
   MPI_Comm_rank(MPI_COMM_WORLD, &me);
+  ME = me;
+  if (getenv("SHARDED_TEST_FAIL_COMPUTE")) FAIL_COMPUTE = atoi(getenv("SHARDED_TEST_FAIL_COMPUTE"));
   const int null_stream = argc > 1 && strcmp(argv[1], "--gpu-host-null") == 0;
   const int host_slabs = null_stream || (argc > 1 && strcmp(argv[1], "--gpu-host") == 0);
   const int gpu = host_slabs || (argc > 1 && strcmp(argv[1], "--gpu") == 0);
@@ -222,7 +228,11 @@ int main(int argc, char** argv) {
           bad += HP[(((size_t) q * mh + slot[m]) * E + i) * W + b] != want_p[m][i * C + q * W + b];
   }
   if (bad) fprintf(stderr, "rank %d: %d parity bytes differ from the oracle\n", me, bad);
-  if (ok && reb) {
+  /* the rebuild is collective: every member runs it or none (as the
+   * backends agree before an exchange) */
+  int enc_ok = ok, all_enc = 0;
+  MPI_Allreduce(&enc_ok, &all_enc, 1, MPI_INT, MPI_LAND, MPI_COMM_WORLD);
+  if (ok && reb && all_enc) {
     /* lose the members, scribble on the gathered slots, rebuild */
     for (int m = 0; m < nm; ++m) {
       int is_lost = 0;

@@ -159,3 +159,22 @@ def test_rebuild_exchange_members_must_agree(tmp_path):
     assert res.returncode != 0
     assert "disagree on the rebuild exchange" in res.stderr, res.stderr
     assert res.stderr.count("backend failed") == 4, res.stderr
+
+
+@pytest.mark.parametrize("scheme,np_,p,e,fail", [("rs", 3, 11, 3, 1), ("rs", 4, 6, 2, 0), ("xor", 3, 5, 1, 2)])
+def test_sharded_compute_failure_keeps_the_exchange_going(scheme, np_, p, e, fail):
+    """One process's compute fails inside the sharded encode: its plan still
+    runs the return exchange its peers are waiting in (sharded.c
+    execute_pipelined / redset_hip_sharded_execute), so every process comes
+    back, the failing one with an error, and the AND of the results fails
+    (src/redset_reedsolomon.c:338-342)."""
+    if not _have():
+        pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", DRIVER, str(p), str(e), "5000"]
+    env = {**os.environ, "SHARDED_TEST_FAIL_COMPUTE": str(fail)}
+    if scheme == "xor":
+        env["SHARDED_TEST_SCHEME"] = "xor"
+    res = run_group(cmd, 60, env=env, cwd="/tmp")
+    assert res.returncode != 0, res.stdout + res.stderr
+    assert f"rank {fail}: encode:" in res.stderr, res.stderr
+    assert "compute callback failed" in res.stderr, res.stderr

@@ -84,13 +84,16 @@ static int rfail(const char* what, ncclResult_t r) {
 static int rccl_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream) {
   struct redset_hip_rccl* R = (struct redset_hip_rccl*) ctx;
   hipStream_t s = (hipStream_t) stream;
+  /* a failed local copy does not skip the peers' messages (they would wait
+   * in their group forever): it is reported after the group */
+  int rc = 0;
   for (int i = 0; i < n; ++i) {
     if (x[i].peer != R->rank) continue;
     /* local copy: the send entry (source) is followed by its receive (destination) */
     if (!x[i].send || i + 1 >= n || x[i + 1].peer != R->rank || x[i + 1].send || x[i + 1].len != x[i].len)
-      return redset_hip_record_error("rccl exchange: malformed local copy");
-    if (hipMemcpyAsync(x[i + 1].buf, x[i].buf, x[i].len, hipMemcpyDeviceToDevice, s) != hipSuccess)
-      return redset_hip_record_error("rccl exchange: local hipMemcpyAsync failed");
+      return redset_hip_record_error("rccl exchange: malformed local copy"); /* a plan bug, on every member */
+    if (!rc && hipMemcpyAsync(x[i + 1].buf, x[i].buf, x[i].len, hipMemcpyDeviceToDevice, s) != hipSuccess)
+      rc = redset_hip_record_error("rccl exchange: local hipMemcpyAsync failed");
     ++i;
   }
   ncclResult_t r = rccl.GroupStart();
@@ -105,7 +108,8 @@ static int rccl_exchange(void* ctx, const redset_hip_xfer* x, int n, void* strea
     }
   }
   r = rccl.GroupEnd();
-  return r == ncclSuccess ? 0 : rfail("ncclGroupEnd", r);
+  if (r != ncclSuccess) return rfail("ncclGroupEnd", r);
+  return rc;
 }
 
 int redset_hip_rccl_available(void) {

@@ -374,3 +374,30 @@ def test_mpi_rank_backends_random(oracle, tmp_path, seed):
             assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
         blob = np.fromfile(reds[r], dtype=np.uint8)
         assert np.array_equal(blob[header[r]:header[r] + e * chunk], want[r]), r
+
+
+def test_mpi_forced_rccl_exchange_on_a_shared_gpu_fails_every_rank(tmp_path):
+    """`redset_hip_rank_set_exchange(SHARDED_RCCL)` with the members sharing
+    the box's one GPU: RCCL refuses the communicator ("Duplicate GPU"), the
+    members agree on that (rank_mpi.c rccl_create's MPI_Allreduce) and every
+    one returns failure before any exchange -- no hang, no partial writes."""
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    tmp = str(tmp_path)
+    p, e = 4, 2
+    rng = np.random.default_rng(5)
+    files, chunk = _setup(tmp, p, p - e, rng, 100_000)
+    reds = [os.path.join(tmp, f"r{r}.rs.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, [128] * p, reds)
+    res = _mpirun(p, ["rs", "encode", e, tmp, 65536])
+    assert res.returncode == 0, res.stdout + res.stderr
+    for path, _ in files[1]:
+        os.unlink(path)
+    os.unlink(reds[1])
+    res = _mpirun(p, ["rs", "rebuild", e, tmp, 65536, 1], timeout=120, env={"RANK_TEST_EXCHANGE": "rccl"})
+    assert res.returncode != 0, res.stdout + res.stderr
+    assert res.stderr.count("backend failed") == p, res.stderr
+    # the driver creates the lost member's files at their recorded sizes
+    # (zeros); nothing was written into them
+    for path, _ in files[1]:
+        assert not os.path.exists(path) or not np.fromfile(path, dtype=np.uint8).any(), path

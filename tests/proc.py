@@ -19,3 +19,15 @@ def run_group(cmd, timeout, env=None, cwd=None):
         out, err = p.communicate()
         pytest.fail(f"timed out after {timeout} s: {' '.join(map(str, cmd))}\n{out[-3000:]}\n{err[-3000:]}")
     return subprocess.CompletedProcess(cmd, p.returncode, out, err)
+
+
+def locked_make(directory, jobs=8, timeout=600):
+    """`make -s -C directory` under an exclusive file lock, so parallel test
+    workers (pytest -n) that need the same build do not relink it under each
+    other."""
+    import fcntl
+
+    with open(os.path.join(directory, ".make.lock"), "w") as lock:
+        fcntl.flock(lock, fcntl.LOCK_EX)
+        return subprocess.run(["make", "-s", f"-j{jobs}", "-C", directory], capture_output=True, text=True,
+                              timeout=timeout)

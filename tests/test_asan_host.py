@@ -18,7 +18,7 @@ import subprocess
 import numpy as np
 import pytest
 
-from proc import run_group
+from proc import locked_make, run_group
 from redset_amd import header as H
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -34,7 +34,7 @@ def asan_build():
         pytest.skip("needs hipcc and ROCm's clang")
     if not os.path.exists(os.path.join(ROOT, "redset_amd", "build", "codec_kernels.o")):
         subprocess.run(["make", "-s", "-j8", "-C", os.path.join(ROOT, "redset_amd", "csrc")], check=True)
-    res = subprocess.run(["make", "-s", "-j8", "-C", ASAN_DIR], capture_output=True, text=True, timeout=600)
+    res = locked_make(ASAN_DIR)
     assert res.returncode == 0, res.stdout + res.stderr
     return BUILD
 

@@ -20,12 +20,13 @@ import subprocess
 import numpy as np
 import pytest
 
-from proc import run_group
+from proc import locked_make, run_group
 from test_gpu_mpi import _logical, _manifests, _setup
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MPI_DIR = os.path.join(ROOT, "tests", "mpi")
-RANK_TEST = os.path.join(MPI_DIR, "build", "rank_test")
+# RANK_TEST_BIN: another build of the driver (tests/asan: host ASan)
+RANK_TEST = os.environ.get("RANK_TEST_BIN") or os.path.join(MPI_DIR, "build", "rank_test")
 STUB = os.path.join(MPI_DIR, "build", "libhipstub.so")
 MPIRUN = "/opt/conda/bin/mpirun"
 
@@ -41,9 +42,12 @@ def stub():
 
 
 def _run(np_, args, env=None, timeout=120):
-    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", "-env", "LD_PRELOAD", STUB, RANK_TEST] + \
-        [str(a) for a in args]
-    return run_group(cmd, timeout, env={**os.environ, **(env or {})})
+    env = {**os.environ, **(env or {})}
+    drv = env.pop("_DRIVER", RANK_TEST)
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", "-env", "LD_PRELOAD", STUB, drv] + [str(a) for a in args]
+    res = run_group(cmd, timeout, env=env)
+    assert "AddressSanitizer" not in res.stderr, res.stderr[-4000:]
+    return res
 
 
 def _stats(stdout, tag="first"):
@@ -161,3 +165,23 @@ def test_host_path_slices_larger_than_buffer(stub, oracle, tmp_path, scheme, p, 
     shapes as a control); parity and rebuilt files must not depend on the
     slice."""
     _round_trip(oracle, str(tmp_path), scheme, p, e, lost, 65536, 31 + p, 20_000_000)
+
+
+ASAN_DRIVER = os.path.join(ROOT, "tests", "asan", "build", "rank_test")
+
+
+@pytest.mark.parametrize("scheme,p,e,lost,buf,maxsize", [("rs", 6, 2, [1, 4], 65536, 200_000),
+                                                          ("rs", 5, 2, [0, 3], 65536, 20_000_000),
+                                                          ("xor", 4, 1, [2], 50000, 200_000)])
+def test_host_path_under_asan(stub, oracle, tmp_path, scheme, p, e, lost, buf, maxsize):
+    """The same host path with the backends' host code built under
+    AddressSanitizer (tests/asan, as tests/test_asan_host.py builds it):
+    round trips, the RS slice rule's large slices, and repeated calls on
+    cached scratch."""
+    if not (os.path.exists("/opt/rocm/bin/hipcc") and os.path.exists("/opt/rocm/lib/llvm/bin/clang")):
+        pytest.skip("needs hipcc and ROCm's clang")
+    res = locked_make(os.path.join(ROOT, "tests", "asan"))
+    assert res.returncode == 0, res.stdout + res.stderr
+    env = {"_DRIVER": ASAN_DRIVER, "RANK_TEST_REPEAT": "2",
+           "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0:exitcode=86"}
+    _round_trip(oracle, str(tmp_path), scheme, p, e, lost, buf, 7 + p, maxsize, env=env)

@@ -572,11 +572,6 @@ out:
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
 }
 
-int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi,
-                              const char* chunk_file, int fd_chunk, size_t chunk_size, size_t buf_size) {
-  const double t0 = stats_begin();
-  return stats_end(t0, rs_encode_impl(rs, comm, lofi, chunk_file, fd_chunk, chunk_size, buf_size));
-}
 
 /* ---- RS decode (replaces redset_reedsolomon_decode, src/redset_reedsolomon.c:570-785) */
 
@@ -841,11 +836,6 @@ out:
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
 }
 
-int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
-                               size_t chunk_size, size_t buf_size) {
-  const double t0 = stats_begin();
-  return stats_end(t0, xor_encode_impl(comm, lofi, chunk_file, fd_chunk, chunk_size, buf_size));
-}
 
 /* ---- XOR decode (replaces redset_xor_decode, src/redset_xor.c:441-531) */
 
@@ -1109,10 +1099,13 @@ static int member_cell(int p, int e, int xor_scheme, int r, int c) {
   return enc < p ? redset_hip_rs_get_data_id(p, e, r, c) : (p - e) + (enc - p);
 }
 
-/* rs == NULL: XOR (e = 1, the root is lost[0]) */
-static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, int e, int missing, const int* lost,
-                          int need_rebuild, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
-                          off_t header, int hrc, size_t chunk_size, size_t B, const redset_hip_transport* tr) {
+/* The encode (encode = 1: every member's data cells in, its parity cells
+ * out) or the rebuild (the lost members' cells) as the sharded plan over a
+ * transport. rs == NULL: XOR (e = 1; rebuild: the root is lost[0]). */
+static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int p, int r, int e, int missing,
+                        const int* lost, int need_rebuild, const redset_hip_io* lofi, const char* chunk_file,
+                        int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B,
+                        const redset_hip_transport* tr) {
   const int d = p - e, ncell = p, world = p;
   const int xor_scheme = rs == NULL;
   size_t win = SHARDED_WINDOW / (size_t) ncell;
@@ -1129,7 +1122,7 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
   const size_t tail = chunk_size - (nwin ? (nwin - 1) * win : 0);
 
   unsigned char* want = calloc((size_t) ncell, 1); /* cells of mine some stripe's decode reads */
-  unsigned char* D = malloc((size_t) missing * p);
+  unsigned char* D = malloc((size_t) (missing > 0 ? missing : 1) * p);
   int* host = malloc(sizeof(int) * (size_t) p);
   int* slot = calloc((size_t) p, sizeof(int));
   scratch S;
@@ -1146,8 +1139,10 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
     if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
   if (!rc && (!want || !D || !host || !slot)) rc = fail("out of host memory");
   if (!rc && need_rebuild && !lofi->write) rc = fail("lofi has no write callback");
-  /* which of my cells the decode reads (the sharded plan sends exactly those) */
-  for (int c = 0; c < p && !rc && !need_rebuild; ++c) {
+  /* which of my cells the exchange reads: the encode every data cell, the
+   * decode those its maps read (the sharded plan sends exactly those) */
+  for (int x = 0; x < d && encode && want; ++x) want[x] = 1;
+  for (int c = 0; c < p && !rc && !need_rebuild && !encode; ++c) {
     int used = xor_scheme;
     if (!xor_scheme) {
       rc = redset_hip_rs_decode_matrix(rs, missing, lost, c, D);
@@ -1170,8 +1165,12 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
       redset_hip_sharded** P = &plan[b][len != win];
       if (!rc && !*P) {
         redset_hip_shard_layout L = {1, host, slot, 1, len, W, hd[b], hp[b], gd[b], gp[b]};
-        rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, tr, NULL, P)
-                        : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, tr, NULL, P);
+        if (encode)
+          rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, tr, NULL, P)
+                          : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, tr, NULL, P);
+        else
+          rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, tr, NULL, P)
+                          : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, tr, NULL, P);
       }
       uint8_t* img = h_img[b];
       for (int x = 0; x < ncell && !rc; ++x) {
@@ -1213,7 +1212,7 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
         g_stats.sent_bytes += info.gather_bytes_sent + info.return_bytes_sent;
         g_stats.recv_bytes += info.gather_bytes_recv + info.return_bytes_recv;
       }
-      for (int x = 0; x < ncell && !rc && need_rebuild; ++x) {
+      for (int x = encode ? d : 0; x < ncell && !rc && (need_rebuild || encode); ++x) {
         const uint8_t* src = x < d ? hd[b] + (size_t) x * W : hp[b] + (size_t) (x - d) * W;
         const size_t spitch = (size_t) (x < d ? d : e) * W;
         if (hipMemcpy2DAsync(img + (size_t) x * WW, W, src, spitch, W, (size_t) world, hipMemcpyDeviceToHost, s) !=
@@ -1223,12 +1222,13 @@ static int decode_sharded(const redset_hip_rs* rs, MPI_Comm comm, int p, int r, 
       }
       if (!rc && hipEventRecord(ev[b], s) != hipSuccess) rc = fail("hipEventRecord failed");
     }
-    /* window n - 1's rebuilt cells, after the header as the host path writes them */
-    if (n >= 1 && need_rebuild && !rc) {
+    /* window n - 1's rebuilt cells (encode: parity cells), after the header
+     * as the host path writes them */
+    if (n >= 1 && (need_rebuild || encode) && !rc) {
       const int pb = 1 - b;
       const size_t poff = (n - 1) * win, plen = n == nwin ? tail : win;
       if (ev_wait(ev[pb])) rc = REDSET_FAILURE;
-      for (int x = 0; x < ncell && !rc; ++x) {
+      for (int x = encode ? d : 0; x < ncell && !rc; ++x) {
         const uint8_t* cell = h_img[pb] + (size_t) x * WW;
         if (x < d) {
           if (io_write(lofi, x, poff, plen, cell) != 0) rc = fail("lofi write failed");
@@ -1282,8 +1282,8 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
                ? rs_decode_host(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
                                 header, hrc, chunk_size, slice_bytes(B, chunk_size, (size_t) (4 * p + 2 * missing)))
-               : decode_sharded(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
-                                header, hrc, chunk_size, B, &tr);
+               : sharded_slot(0, rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
+                              header, hrc, chunk_size, B, &tr);
   redset_hip_mpi_transport_destroy(mt);
   return stats_end(t0, rc);
 }
@@ -1312,10 +1312,64 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   g_last_exchange = mode;
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
                ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B)
-               : decode_sharded(NULL, comm, p, r, 1, 1, &root, r == root, lofi, chunk_file, fd_chunk, header, hrc,
-                                chunk_size, B, &tr);
+               : sharded_slot(0, NULL, comm, p, r, 1, 1, &root, r == root, lofi, chunk_file, fd_chunk, header, hrc,
+                              chunk_size, B, &tr);
   redset_hip_mpi_transport_destroy(mt);
   return stats_end(t0, rc);
+}
+
+/* The encodes pick their exchange as the decodes do (choose_exchange): on a
+ * node whose members each own a GPU the encode runs as the sharded plan over
+ * RCCL -- every data cell's column slices gathered onto the GPUs, gf_mac (or
+ * the XOR) there, the parity slices returned to their holders -- instead of
+ * the host ring (src/redset_reedsolomon.c:329-377, src/redset_xor.c:251-285). */
+static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file,
+                       int fd_chunk, size_t chunk_size, size_t buf_size) {
+  int p, r, e = 1;
+  if (!lofi || !lofi->read) return fail("encode_rank: null argument");
+  if (comm_geometry(comm, &p, &r)) return REDSET_FAILURE;
+  if (rs) {
+    int rp;
+    if (redset_hip_rs_shape(rs, &rp, &e)) return REDSET_FAILURE;
+    if (p != rp) return fail("communicator has %d ranks, codec %d", p, rp);
+  } else if (p < 2) {
+    return fail("XOR needs at least 2 ranks");
+  }
+  const size_t B = buf_size ? buf_size : DEFAULT_BUF;
+  if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
+  int mode;
+  redset_hip_transport tr;
+  redset_hip_mpi_transport* mt = NULL;
+  if (choose_exchange(comm, p, r, &mode, &tr, &mt)) {
+    redset_hip_mpi_transport_destroy(mt);
+    return REDSET_FAILURE;
+  }
+  g_last_exchange = mode;
+  int rc;
+  if (mode == REDSET_HIP_EXCHANGE_HOST_MPI) {
+    rc = rs ? rs_encode_impl(rs, comm, lofi, chunk_file, fd_chunk, chunk_size, buf_size)
+            : xor_encode_impl(comm, lofi, chunk_file, fd_chunk, chunk_size, buf_size);
+  } else {
+    /* a bad fd on one member is agreed on inside, not returned early */
+    off_t header;
+    const int hrc = header_size(fd_chunk, chunk_file, &header);
+    rc = sharded_slot(1, rs, comm, p, r, e, 0, NULL, 0, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B, &tr);
+  }
+  redset_hip_mpi_transport_destroy(mt);
+  return rc;
+}
+
+int redset_hip_rs_encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi,
+                              const char* chunk_file, int fd_chunk, size_t chunk_size, size_t buf_size) {
+  const double t0 = stats_begin();
+  if (!rs) return stats_end(t0, fail("rs_encode_rank: null argument"));
+  return stats_end(t0, encode_rank(rs, comm, lofi, chunk_file, fd_chunk, chunk_size, buf_size));
+}
+
+int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file, int fd_chunk,
+                               size_t chunk_size, size_t buf_size) {
+  const double t0 = stats_begin();
+  return stats_end(t0, encode_rank(NULL, comm, lofi, chunk_file, fd_chunk, chunk_size, buf_size));
 }
 
 /* ---- MPI transport of the sharded path (include/redset_hip_mpi.h) ------- */

@@ -190,7 +190,8 @@ int main(int argc, char** argv) {
   double dt = MPI_Wtime() - t0, dmax = 0;
   MPI_Reduce(&dt, &dmax, 1, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
   if (rank == 0) printf("rank_test: %s %s %d ranks chunk %llu buf %zu: %.4f s\n", argv[1], argv[2], ranks, chunk, buf, dmax);
-  if (rank == 0 && !encode) printf("rank_test: rebuild exchange %s\n", exchange_name(redset_hip_rank_last_exchange()));
+  if (rank == 0)
+    printf("rank_test: %s exchange %s\n", encode ? "encode" : "rebuild", exchange_name(redset_hip_rank_last_exchange()));
   print_stats(rank, "first");
 
   const char* rep = getenv("RANK_TEST_REPEAT");

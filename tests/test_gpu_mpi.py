@@ -60,9 +60,9 @@ def _exchange_env(exchange):
     return {"RANK_TEST_EXCHANGE": exchange}
 
 
-def _check_exchange(res, exchange):
+def _check_exchange(res, exchange, op="rebuild"):
     used = "host" if exchange == "auto" else exchange.replace("-windows", "")
-    assert f"rebuild exchange {used}" in res.stdout, res.stdout
+    assert f"{op} exchange {used}" in res.stdout, res.stdout
 
 
 def _setup(tmp, p, d, rng, maxsize):
@@ -111,8 +111,9 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf, exchange):
     _manifests(tmp, files, chunk, header, reds)
     crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
 
-    res = _mpirun(p, [scheme, "encode", e, tmp, buf])
+    res = _mpirun(p, [scheme, "encode", e, tmp, buf], env=_exchange_env(exchange))
     assert res.returncode == 0, res.stdout + res.stderr
+    _check_exchange(res, exchange, "encode")
     lofi = [_logical(fl, d * chunk) for fl in files]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     if scheme == "rs":
@@ -161,6 +162,13 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf, exchange):
     ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "3", "RANK_TEST_EXCHANGE": "sharded-mpi",
                         "REDSET_HIP_TEST_SHARDED_WINDOW": "65536"}),
     ("rs", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "0", "RANK_TEST_EXCHANGE": "sharded-mpi"}),
+    # the encodes through the sharded exchange (the path a node with a GPU
+    # per member takes over RCCL)
+    ("rs", "encode", {"RANK_TEST_FAIL_READ": "2", "RANK_TEST_EXCHANGE": "sharded-mpi"}),
+    ("rs", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "1", "RANK_TEST_EXCHANGE": "sharded-mpi",
+                      "REDSET_HIP_TEST_SHARDED_WINDOW": "65536"}),
+    ("xor", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "3", "RANK_TEST_EXCHANGE": "sharded-mpi",
+                       "REDSET_HIP_TEST_SHARDED_WINDOW": "65536"}),
 ])
 def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme, op, env):
     """One member's I/O or device error in the middle of the loop: that member
@@ -243,8 +251,9 @@ def test_mpi_config0_xor_4_ranks_16MiB(oracle, tmp_path, exchange):
     header = [4096] * p
     reds = [os.path.join(tmp, f"r{r}.xor.redset") for r in range(p)]
     _manifests(tmp, files, chunk, header, reds)
-    res = _mpirun(p, ["xor", "encode", e, tmp, 1 << 20])
+    res = _mpirun(p, ["xor", "encode", e, tmp, 1 << 20], env=_exchange_env(exchange))
     assert res.returncode == 0, res.stdout + res.stderr
+    _check_exchange(res, exchange, "encode")
     lofi = [_logical(fl, (p - 1) * chunk) for fl in files]
     want = [np.zeros(chunk, np.uint8) for _ in range(p)]
     oracle.xor_encode_set(p, lofi, want, chunk)
@@ -301,10 +310,11 @@ def test_mpi_rank_backends_repeated_calls(oracle, tmp_path, scheme, p, e, lost, 
     reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
     _manifests(tmp, files, chunk, header, reds)
     crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
-    env = {**os.environ, "RANK_TEST_REPEAT": "3"}
+    env = {**os.environ, "RANK_TEST_REPEAT": "3", **_exchange_env(exchange)}
     cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST, scheme, "encode", str(e), tmp, "32768"]
     res = run_group(cmd, 120, env=env)
     assert res.returncode == 0 and "call 3 of 3" in res.stdout, res.stdout + res.stderr
+    _check_exchange(res, exchange, "encode")
     lofi = [_logical(fl, d * chunk) for fl in files]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     if scheme == "rs":
@@ -350,8 +360,10 @@ def test_mpi_rank_backends_random(oracle, tmp_path, seed):
     reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
     _manifests(tmp, files, chunk, header, reds)
     crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
-    res = _mpirun(p, [scheme, "encode", e, tmp, buf], timeout=120)
-    assert res.returncode == 0, (scheme, p, e, buf, res.stdout + res.stderr)
+    exchange = EXCHANGES[seed % 3]
+    res = _mpirun(p, [scheme, "encode", e, tmp, buf], timeout=120, env=_exchange_env(exchange))
+    assert res.returncode == 0, (scheme, p, e, buf, exchange, res.stdout + res.stderr)
+    _check_exchange(res, exchange, "encode")
     lofi = [_logical(fl, d * chunk) for fl in files]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     if scheme == "rs":
@@ -364,7 +376,6 @@ def test_mpi_rank_backends_random(oracle, tmp_path, seed):
         for path, _ in files[r]:
             os.unlink(path)
         os.unlink(reds[r])
-    exchange = EXCHANGES[seed % 3]
     res = _mpirun(p, [scheme, "rebuild", e, tmp, buf] + lost, timeout=120, env=_exchange_env(exchange))
     assert res.returncode == 0, (scheme, p, e, buf, lost, exchange, res.stdout + res.stderr)
     _check_exchange(res, exchange)

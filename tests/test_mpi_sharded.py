@@ -119,8 +119,9 @@ def _rank_test_set(tmp, p, chunk):
             f.write(b"H" * 64 + bytes(chunk * 2))
 
 
+@pytest.mark.parametrize("op", ["rebuild", "encode"])
 @pytest.mark.parametrize("exchange,used", [("", "host"), ("host", "host"), ("sharded-mpi", "sharded-mpi")])
-def test_rebuild_exchange_choice_on_cpu(tmp_path, exchange, used):
+def test_rebuild_exchange_choice_on_cpu(tmp_path, exchange, used, op):
     """The per-rank decode's exchange choice (rank_mpi.c choose_exchange) is
     collective and agreed before any exchange: on a machine without a GPU,
     "auto" finds no GPU per member and takes the host path, a forced mode is
@@ -138,10 +139,11 @@ def test_rebuild_exchange_choice_on_cpu(tmp_path, exchange, used):
     env.pop("RANK_TEST_EXCHANGE", None)
     if exchange:
         env["RANK_TEST_EXCHANGE"] = exchange
-    cmd = [MPIRUN, "-np", "4", "-host", "localhost", RANK_TEST, "rs", "rebuild", "2", tmp, "4096", "1", "2"]
+    cmd = [MPIRUN, "-np", "4", "-host", "localhost", RANK_TEST, "rs", op, "2", tmp, "4096"] + \
+        (["1", "2"] if op == "rebuild" else [])
     res = run_group(cmd, 60, env=env, cwd="/tmp")
     assert res.returncode != 0
-    assert f"rebuild exchange {used}" in res.stdout, res.stdout + res.stderr
+    assert f"{op} exchange {used}" in res.stdout, res.stdout + res.stderr
     assert res.stderr.count("backend failed") == 4, res.stderr
 
 

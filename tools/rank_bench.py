@@ -119,7 +119,7 @@ def main():
             calls = [float(x) for x in re.findall(r"call \d+ of \d+(?: \(warm\))?: ([0-9.]+) s", res.stdout)]
             tw = float(np.median(calls))
             out[op].update(warm_seconds=tw, warm_GBps=round(alg / tw / 1e9, 3), warm_calls=calls)
-        ex = re.search(r"rebuild exchange (\S+)", res.stdout)
+        ex = re.search(op + r" exchange (\S+)", res.stdout)
         if ex:
             out[op]["exchange"] = ex.group(1)
         tag = "warm" if warm else "first"

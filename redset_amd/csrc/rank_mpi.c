@@ -839,42 +839,61 @@ out:
 
 /* ---- XOR decode (replaces redset_xor_decode, src/redset_xor.c:441-531) */
 
-/* the host-MPI exchange of the XOR decode: every survivor's cell of stripe c
- * to the root, stripe by stripe */
+/* The host-MPI exchange of the XOR decode: a chain through the survivors,
+ * as the reference's pipelined reduce to the root (src/redset_xor.c:466-524),
+ * but a slice of every stripe per message. Survivors in order root+1,
+ * root+2, ..., root-1: the first sends its p cells of slice n (its data
+ * segments and its parity, one per stripe) to the next; each following one
+ * XORs what it receives with its own cells on the GPU and passes the result
+ * on; the root receives, for every stripe, the XOR of every survivor's cell
+ * -- its own lost cell -- and writes it. Every member sends and receives
+ * p cells per slice, where a gather to the root would make the root receive
+ * (p-1)*p. After a read or device error a member sends zeros and keeps the
+ * chain going (src/redset_xor.c:466-524 keeps its loop going too), returning
+ * failure. */
 static int xor_decode_host(MPI_Comm comm, int p, int r, int root, const redset_hip_io* lofi, const char* chunk_file,
-                           int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B) {
-
-  const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
-  MPI_Request* req = malloc(sizeof(*req) * (size_t) p);
+                           int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t buf) {
+  /* a message carries a slice of all p stripes: keep it within an MPI count
+   * (the slice never changes the bytes written) */
+  const size_t B = buf > (size_t) INT_MAX / (size_t) p ? (size_t) INT_MAX / (size_t) p : buf;
+  const int pos = (r - root - 1 + p) % p; /* survivors 0 .. p-2, the root p-1 */
+  const int prev = pos > 0 ? (r - 1 + p) % p : -1;
+  const int next = pos < p - 1 ? (r + 1) % p : -1;
+  const int survivor = next >= 0, compute = prev >= 0 && next >= 0;
+  const size_t slab = (size_t) p * B; /* a slice of every stripe, cell c at c * count */
   scratch S;
   scratch_init(&S);
-  /* the root double-buffers: unit n's cells arrive while the GPU XORs unit
-   * n-1, whose result is written after */
-  uint8_t* h_cells[2] = {scratch_host(&S, (size_t) p * B), scratch_host(&S, (size_t) p * B)};
-  uint8_t* h_out[2] = {scratch_host(&S, B), scratch_host(&S, B)};
-  uint8_t* d_cells[2] = {scratch_dev(&S, (size_t) p * B), scratch_dev(&S, (size_t) p * B)};
-  uint8_t* d_out[2] = {scratch_dev(&S, B), scratch_dev(&S, B)};
-  hipEvent_t ev_done[2] = {NULL, NULL};
+  uint8_t* h_own[2] = {NULL, NULL};
+  uint8_t* h_in[2] = {NULL, NULL};
+  uint8_t* h_res[2] = {NULL, NULL};
+  uint8_t* d_own[2] = {NULL, NULL};
+  uint8_t* d_in[2] = {NULL, NULL};
+  for (int k = 0; k < 2; ++k) {
+    if (survivor) h_own[k] = scratch_host(&S, slab);
+    if (prev >= 0) h_in[k] = scratch_host(&S, slab);
+    if (compute) {
+      h_res[k] = scratch_host(&S, slab);
+      d_own[k] = scratch_dev(&S, slab);
+      d_in[k] = scratch_dev(&S, slab);
+    }
+  }
+  hipEvent_t ev_done = NULL;
   int rc = S.rc ? S.rc : hrc;
-  for (int k = 0; k < 2 && !rc; ++k)
-    if (hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
-  if (!rc && (!ins || !req)) rc = fail("out of host memory");
+  if (!rc && compute && hipEventCreateWithFlags(&ev_done, hipEventDisableTiming) != hipSuccess)
+    rc = fail("hipEventCreate failed");
   if ((rc = agree_setup(comm, rc))) goto out;
-  int dev_failed = 0; /* root: keep receiving every cell, skip GPU work and writes */
-  int have_prev = 0, prev_b = 0, prev_c = 0;
-  size_t prev_nread = 0, prev_count = 0;
-  long n = 0;
-
-  /* stripe by stripe, as the reference's pipelined reduce to the root
-   * (src/redset_xor.c:466-524): every survivor sends its cell of stripe c,
-   * the root XORs them on the GPU and writes its own cell of stripe c */
-  for (int c = 0; c <= p; ++c) {
-    for (size_t nread = 0; c == p ? nread == 0 : nread < chunk_size; nread += B, ++n) {
-      const int more = c < p;  /* c == p: one last pass to write the final unit */
-      const size_t count = more ? min_sz(B, chunk_size - nread) : 0;
-      const int bb = (int) (n & 1);
-      if (more && r != root) {
-        uint8_t* mine = h_cells[0] + (size_t) r * B;
+  MPI_Request rreq[2] = {MPI_REQUEST_NULL, MPI_REQUEST_NULL}, sreq[2] = {MPI_REQUEST_NULL, MPI_REQUEST_NULL};
+  int dev_failed = 0;
+  const size_t nslice = (chunk_size + B - 1) / B;
+  for (size_t n = 0; n < nslice; ++n) {
+    const int b = (int) (n & 1);
+    const size_t nread = n * B, count = min_sz(B, chunk_size - nread), bytes = (size_t) p * count;
+    if (prev >= 0) irecv(h_in[b], (int) bytes, prev, 0, comm, &rreq[b]);
+    if (survivor) {
+      /* the first survivor sends h_own[b] itself: slice n-2's send is done */
+      if (prev < 0) mpi_waitall(1, &sreq[b]);
+      for (int c = 0; c < p; ++c) {
+        uint8_t* mine = h_own[b] + (size_t) c * count;
         int bad;
         if (c != r) {
           bad = io_read(lofi, xor_segment(r, c), nread, count, mine) != 0;
@@ -884,60 +903,49 @@ static int xor_decode_host(MPI_Comm comm, int p, int r, int root, const redset_h
           if (bad) rc = fail("read %s failed", chunk_file);
         }
         if (bad) memset(mine, 0, count);
-        const double t0 = now_s();
-        MPI_Send(mine, (int) count, MPI_BYTE, root, 0, comm);
-        g_stats.mpi_seconds += now_s() - t0;
-        g_stats.sent_bytes += count;
-        continue;
       }
-      if (r != root) continue;
-      if (more) {
-        /* h_cells[bb] was last read by unit n-2's copy, waited for when
-         * unit n-2 was written (below, during unit n-1) */
-        int k = 0;
-        for (int t = 0; t < p; ++t)
-          if (t != root) irecv(h_cells[bb] + (size_t) t * B, (int) count, t, 0, comm, &req[k++]);
-        mpi_waitall(k, req);
-        if (!dev_failed) {
-          int nin = 0;
-          for (int t = 0; t < p; ++t)
-            if (t != root) ins[nin++] = d_cells[bb] + (size_t) t * B;
-          int grc = injected_device_failure(comm);
-          if (!grc) grc = h2d(&S, d_cells[bb], h_cells[bb], (size_t) p * B);
-          if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out[bb], count, 0, S.stream);
-          if (!grc) grc = d2h(&S, h_out[bb], d_out[bb], count);
-          if (!grc) grc = ev_record(&S, ev_done[bb]);
-          if (grc) {
-            rc = grc;
-            dev_failed = 1;
-          }
-        }
-      }
-      if (have_prev && !dev_failed) {
-        if (ev_wait(ev_done[prev_b])) {
-          rc = REDSET_FAILURE;
-          dev_failed = 1;
-        } else if (prev_c != root) {
-          if (io_write(lofi, xor_segment(root, prev_c), prev_nread,
-                                          prev_count, h_out[prev_b]) != 0)
-            rc = fail("lofi write failed");
-        } else if (pwrite_full(fd_chunk, h_out[prev_b], prev_count, header + (off_t) prev_nread) != 0) {
+    }
+    if (prev < 0) {
+      isend(h_own[b], (int) bytes, next, 0, comm, &sreq[b]);
+      continue;
+    }
+    mpi_waitall(1, &rreq[b]);
+    if (next < 0) {
+      /* the root: stripe c's XOR of every survivor's cell is its own cell */
+      for (int c = 0; c < p; ++c) {
+        const uint8_t* cell = h_in[b] + (size_t) c * count;
+        if (c != root) {
+          if (io_write(lofi, xor_segment(root, c), nread, count, cell) != 0) rc = fail("lofi write failed");
+        } else if (pwrite_full(fd_chunk, cell, count, header + (off_t) nread) != 0) {
           rc = fail("write %s failed", chunk_file);
         }
       }
-      have_prev = more;
-      prev_b = bb;
-      prev_c = c;
-      prev_nread = nread;
-      prev_count = count;
+      continue;
     }
+    /* h_res[b] is free once slice n-2's send is done */
+    mpi_waitall(1, &sreq[b]);
+    int grc = dev_failed ? REDSET_FAILURE : injected_device_failure(comm);
+    if (!grc) grc = h2d(&S, d_own[b], h_own[b], bytes);
+    if (!grc) grc = h2d(&S, d_in[b], h_in[b], bytes);
+    if (!grc) {
+      const unsigned char* in1[1] = {d_in[b]};
+      grc = redset_hip_xor_combine(in1, 1, d_own[b], bytes, 1, S.stream);
+    }
+    if (!grc) grc = d2h(&S, h_res[b], d_own[b], bytes);
+    if (!grc) grc = ev_record(&S, ev_done);
+    if (!grc) grc = ev_wait(ev_done);
+    if (grc) {
+      if (!dev_failed) rc = rc ? rc : grc;
+      dev_failed = 1;
+      memset(h_res[b], 0, bytes);
+    }
+    isend(h_res[b], (int) bytes, next, 0, comm, &sreq[b]);
   }
+  mpi_waitall(2, sreq);
+  mpi_waitall(2, rreq);
 out:
   scratch_free(&S, rc == 0);
-  for (int k = 0; k < 2; ++k)
-    if (ev_done[k]) (void) hipEventDestroy(ev_done[k]);
-  free(ins);
-  free(req);
+  if (ev_done) (void) hipEventDestroy(ev_done);
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
 }
 

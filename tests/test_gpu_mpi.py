@@ -147,7 +147,8 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf, exchange):
     ("rs", "rebuild", {"RANK_TEST_FAIL_READ": "3"}),
     ("rs", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "0"}),
     ("xor", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2"}),
-    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2"}),  # the root runs the GPU work
+    # the chain's middle survivors run the GPU work (lost [2]: chain 3 -> 0 -> 1 -> root 2)
+    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "1"}),
     ("xor", "rebuild", {"RANK_TEST_FAIL_READ": "0"}),
     # the sharded exchange: every member's state is agreed on before each
     # window's exchange, so one member's error stops all of them

@@ -839,6 +839,112 @@ out:
 
 /* ---- XOR decode (replaces redset_xor_decode, src/redset_xor.c:441-531) */
 
+#define XOR_CHAIN_SLICES_PER_HOP 4
+
+/* The XOR decode's gather to the root: every survivor sends its cell of
+ * stripe c straight to the root (blocking sends, stripe by stripe), the root
+ * XORs them on the GPU and writes its own cell of stripe c. One message per
+ * cell, no hops: the shorter call when the chunk spans few slices. */
+static int xor_decode_gather(MPI_Comm comm, int p, int r, int root, const redset_hip_io* lofi, const char* chunk_file,
+                           int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B) {
+
+  const unsigned char** ins = malloc(sizeof(*ins) * (size_t) p);
+  MPI_Request* req = malloc(sizeof(*req) * (size_t) p);
+  scratch S;
+  scratch_init(&S);
+  /* the root double-buffers: unit n's cells arrive while the GPU XORs unit
+   * n-1, whose result is written after */
+  uint8_t* h_cells[2] = {scratch_host(&S, (size_t) p * B), scratch_host(&S, (size_t) p * B)};
+  uint8_t* h_out[2] = {scratch_host(&S, B), scratch_host(&S, B)};
+  uint8_t* d_cells[2] = {scratch_dev(&S, (size_t) p * B), scratch_dev(&S, (size_t) p * B)};
+  uint8_t* d_out[2] = {scratch_dev(&S, B), scratch_dev(&S, B)};
+  hipEvent_t ev_done[2] = {NULL, NULL};
+  int rc = S.rc ? S.rc : hrc;
+  for (int k = 0; k < 2 && !rc; ++k)
+    if (hipEventCreateWithFlags(&ev_done[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
+  if (!rc && (!ins || !req)) rc = fail("out of host memory");
+  if ((rc = agree_setup(comm, rc))) goto out;
+  int dev_failed = 0; /* root: keep receiving every cell, skip GPU work and writes */
+  int have_prev = 0, prev_b = 0, prev_c = 0;
+  size_t prev_nread = 0, prev_count = 0;
+  long n = 0;
+
+  /* stripe by stripe, as the reference's pipelined reduce to the root
+   * (src/redset_xor.c:466-524): every survivor sends its cell of stripe c,
+   * the root XORs them on the GPU and writes its own cell of stripe c */
+  for (int c = 0; c <= p; ++c) {
+    for (size_t nread = 0; c == p ? nread == 0 : nread < chunk_size; nread += B, ++n) {
+      const int more = c < p;  /* c == p: one last pass to write the final unit */
+      const size_t count = more ? min_sz(B, chunk_size - nread) : 0;
+      const int bb = (int) (n & 1);
+      if (more && r != root) {
+        uint8_t* mine = h_cells[0] + (size_t) r * B;
+        int bad;
+        if (c != r) {
+          bad = io_read(lofi, xor_segment(r, c), nread, count, mine) != 0;
+          if (bad) rc = fail("lofi read failed");
+        } else {
+          bad = pread_full(fd_chunk, mine, count, header + (off_t) nread) != 0;
+          if (bad) rc = fail("read %s failed", chunk_file);
+        }
+        if (bad) memset(mine, 0, count);
+        const double t0 = now_s();
+        MPI_Send(mine, (int) count, MPI_BYTE, root, 0, comm);
+        g_stats.mpi_seconds += now_s() - t0;
+        g_stats.sent_bytes += count;
+        continue;
+      }
+      if (r != root) continue;
+      if (more) {
+        /* h_cells[bb] was last read by unit n-2's copy, waited for when
+         * unit n-2 was written (below, during unit n-1) */
+        int k = 0;
+        for (int t = 0; t < p; ++t)
+          if (t != root) irecv(h_cells[bb] + (size_t) t * B, (int) count, t, 0, comm, &req[k++]);
+        mpi_waitall(k, req);
+        if (!dev_failed) {
+          int nin = 0;
+          for (int t = 0; t < p; ++t)
+            if (t != root) ins[nin++] = d_cells[bb] + (size_t) t * B;
+          int grc = injected_device_failure(comm);
+          if (!grc) grc = h2d(&S, d_cells[bb], h_cells[bb], (size_t) p * B);
+          if (!grc) grc = redset_hip_xor_combine(ins, nin, d_out[bb], count, 0, S.stream);
+          if (!grc) grc = d2h(&S, h_out[bb], d_out[bb], count);
+          if (!grc) grc = ev_record(&S, ev_done[bb]);
+          if (grc) {
+            rc = grc;
+            dev_failed = 1;
+          }
+        }
+      }
+      if (have_prev && !dev_failed) {
+        if (ev_wait(ev_done[prev_b])) {
+          rc = REDSET_FAILURE;
+          dev_failed = 1;
+        } else if (prev_c != root) {
+          if (io_write(lofi, xor_segment(root, prev_c), prev_nread,
+                                          prev_count, h_out[prev_b]) != 0)
+            rc = fail("lofi write failed");
+        } else if (pwrite_full(fd_chunk, h_out[prev_b], prev_count, header + (off_t) prev_nread) != 0) {
+          rc = fail("write %s failed", chunk_file);
+        }
+      }
+      have_prev = more;
+      prev_b = bb;
+      prev_c = c;
+      prev_nread = nread;
+      prev_count = count;
+    }
+  }
+out:
+  scratch_free(&S, rc == 0);
+  for (int k = 0; k < 2; ++k)
+    if (ev_done[k]) (void) hipEventDestroy(ev_done[k]);
+  free(ins);
+  free(req);
+  return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
 /* The host-MPI exchange of the XOR decode: a chain through the survivors,
  * as the reference's pipelined reduce to the root (src/redset_xor.c:466-524),
  * but a slice of every stripe per message. Survivors in order root+1,
@@ -851,8 +957,8 @@ out:
  * (p-1)*p. After a read or device error a member sends zeros and keeps the
  * chain going (src/redset_xor.c:466-524 keeps its loop going too), returning
  * failure. */
-static int xor_decode_host(MPI_Comm comm, int p, int r, int root, const redset_hip_io* lofi, const char* chunk_file,
-                           int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t buf) {
+static int xor_decode_chain(MPI_Comm comm, int p, int r, int root, const redset_hip_io* lofi, const char* chunk_file,
+                            int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t buf) {
   /* a message carries a slice of all p stripes: keep it within an MPI count
    * (the slice never changes the bytes written) */
   const size_t B = buf > (size_t) INT_MAX / (size_t) p ? (size_t) INT_MAX / (size_t) p : buf;
@@ -947,6 +1053,23 @@ out:
   scratch_free(&S, rc == 0);
   if (ev_done) (void) hipEventDestroy(ev_done);
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+/* The host-MPI exchange of the XOR decode: the chain when the chunk spans
+ * enough slices to fill it, else the gather (measured crossover,
+ * profiles/r04s21_xor_decode_order.txt). Every member derives the same
+ * choice from the same arguments. */
+static int xor_decode_host(MPI_Comm comm, int p, int r, int root, const redset_hip_io* lofi, const char* chunk_file,
+                           int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B) {
+  const size_t nslice = (chunk_size + B - 1) / B;
+  int chain = nslice >= (size_t) XOR_CHAIN_SLICES_PER_HOP * (size_t) (p - 1);
+#if REDSET_HIP_TEST_KNOBS
+  /* test builds: REDSET_HIP_TEST_XOR_DECODE=gather|chain forces one (A/B runs, tests) */
+  const char* v = getenv("REDSET_HIP_TEST_XOR_DECODE");
+  if (v) chain = strcmp(v, "chain") == 0;
+#endif
+  return chain ? xor_decode_chain(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B)
+               : xor_decode_gather(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B);
 }
 
 /* ---- the multi-rank rebuild over the sharded plan (RCCL / xGMI) ---------- */

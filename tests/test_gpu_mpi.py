@@ -147,8 +147,12 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf, exchange):
     ("rs", "rebuild", {"RANK_TEST_FAIL_READ": "3"}),
     ("rs", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "0"}),
     ("xor", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2"}),
-    # the chain's middle survivors run the GPU work (lost [2]: chain 3 -> 0 -> 1 -> root 2)
-    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "1"}),
+    # small chunks take the gather to the root, which runs the GPU work
+    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "2"}),
+    # the chain (forced: test twin) runs it on its middle survivors
+    # (lost [2]: chain 3 -> 0 -> 1 -> root 2)
+    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "1", "REDSET_HIP_TEST_XOR_DECODE": "chain"}),
+    ("xor", "rebuild", {"RANK_TEST_FAIL_READ": "3", "REDSET_HIP_TEST_XOR_DECODE": "chain"}),
     ("xor", "rebuild", {"RANK_TEST_FAIL_READ": "0"}),
     # the sharded exchange: every member's state is agreed on before each
     # window's exchange, so one member's error stops all of them
@@ -413,3 +417,35 @@ def test_mpi_forced_rccl_exchange_on_a_shared_gpu_fails_every_rank(tmp_path):
     # (zeros); nothing was written into them
     for path, _ in files[1]:
         assert not os.path.exists(path) or not np.fromfile(path, dtype=np.uint8).any(), path
+
+
+@pytest.mark.parametrize("order", ["chain", "gather"])
+@pytest.mark.parametrize("p,lost,buf", [(2, 0, 4096), (3, 2, 65536), (5, 1, 40000), (8, 6, 100_003)])
+def test_mpi_xor_decode_orders(oracle, tmp_path, order, p, lost, buf):
+    """Both host orders of the XOR rebuild (rank_mpi.c xor_decode_host: the
+    chain through the survivors, the gather to the root), forced through the
+    test twin whatever the chunk size picks: rebuilt files by CRC32 and the
+    root's parity bytes against the oracle."""
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    tmp = str(tmp_path)
+    rng = np.random.default_rng(600 + p)
+    files, chunk = _setup(tmp, p, p - 1, rng, 300_000)
+    header = [int(rng.integers(0, 3000)) for _ in range(p)]
+    reds = [os.path.join(tmp, f"r{r}.xor.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, header, reds)
+    crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for path, _ in files[lost]}
+    res = _mpirun(p, ["xor", "encode", 1, tmp, buf])
+    assert res.returncode == 0, res.stdout + res.stderr
+    want = np.fromfile(reds[lost], dtype=np.uint8)[header[lost]:].copy()
+    for path, _ in files[lost]:
+        os.unlink(path)
+    os.unlink(reds[lost])
+    ld = os.environ.get("LD_LIBRARY_PATH")
+    env = {"REDSET_HIP_TEST_XOR_DECODE": order, "LD_LIBRARY_PATH": TWIN_DIR + (":" + ld if ld else "")}
+    res = _mpirun(p, ["xor", "rebuild", 1, tmp, buf, lost], env=env)
+    assert res.returncode == 0, res.stdout + res.stderr
+    for path, size in files[lost]:
+        assert os.path.getsize(path) == size
+        assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
+    assert np.array_equal(np.fromfile(reds[lost], dtype=np.uint8)[header[lost]:], want)

@@ -185,3 +185,22 @@ def test_host_path_under_asan(stub, oracle, tmp_path, scheme, p, e, lost, buf, m
     env = {"_DRIVER": ASAN_DRIVER, "RANK_TEST_REPEAT": "2",
            "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0:exitcode=86"}
     _round_trip(oracle, str(tmp_path), scheme, p, e, lost, buf, 7 + p, maxsize, env=env)
+
+
+TWIN_DIR = os.path.join(ROOT, "redset_amd", "lib_test")
+
+
+@pytest.mark.parametrize("order", ["chain", "gather"])
+@pytest.mark.parametrize("p,lost,buf", [(2, [0], 4096), (3, [2], 65536), (6, [1], 40000), (8, [7], 100_003)])
+def test_host_path_xor_decode_orders(stub, oracle, tmp_path, order, p, lost, buf):
+    """Both orders of the XOR host decode (the chain through the survivors,
+    the gather to the root), forced through the test twin's backends."""
+    if not os.path.exists(os.path.join(TWIN_DIR, "libredset_hip_mpi.so")):
+        pytest.skip("test twin not built")
+    ld = os.environ.get("LD_LIBRARY_PATH")
+    env = {"REDSET_HIP_TEST_XOR_DECODE": order, "LD_LIBRARY_PATH": TWIN_DIR + (":" + ld if ld else "")}
+    _, reb, chunk = _round_trip(oracle, str(tmp_path), "xor", p, 1, lost, buf, 900 + p, 300_000, env=env)
+    # the busiest receiver: every member gets p cells in the chain, the root
+    # (p - 1) * p in the gather
+    got = _stats(reb.stdout)["recv_bytes"][0]
+    assert got == (p if order == "chain" else (p - 1) * p) * chunk, (got, chunk)

@@ -839,7 +839,8 @@ out:
 
 /* ---- XOR decode (replaces redset_xor_decode, src/redset_xor.c:441-531) */
 
-#define XOR_CHAIN_SLICES_PER_HOP 4
+#define XOR_CHAIN_SLICES_PER_HOP 4 /* the chain: at least this many slices per hop ... */
+#define XOR_CHAIN_MIN_RANKS 6      /* ... and this many members (xor_decode_host) */
 
 /* The XOR decode's gather to the root: every survivor sends its cell of
  * stripe c straight to the root (blocking sends, stripe by stripe), the root
@@ -1055,14 +1056,17 @@ out:
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
 }
 
-/* The host-MPI exchange of the XOR decode: the chain when the chunk spans
- * enough slices to fill it, else the gather (measured crossover,
- * profiles/r04s21_xor_decode_order.txt). Every member derives the same
+/* The host-MPI exchange of the XOR decode: the chain for wide sets whose
+ * chunk spans enough slices to fill it, else the gather. Measured on one box
+ * (1 MiB buffers, profiles/r04s21_xor_decode_order.txt): at p = 4 the gather
+ * wins at every chunk size (5.3-64 MiB: 2.2-2.5x), at p = 8 it wins at 8 MiB
+ * (1.3x) and loses at 32 and 64 MiB (chain 1.45x and 1.75x faster), where
+ * the root's (p-1)*p cells per slice swamp it. Every member derives the same
  * choice from the same arguments. */
 static int xor_decode_host(MPI_Comm comm, int p, int r, int root, const redset_hip_io* lofi, const char* chunk_file,
                            int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B) {
   const size_t nslice = (chunk_size + B - 1) / B;
-  int chain = nslice >= (size_t) XOR_CHAIN_SLICES_PER_HOP * (size_t) (p - 1);
+  int chain = p >= XOR_CHAIN_MIN_RANKS && nslice >= (size_t) XOR_CHAIN_SLICES_PER_HOP * (size_t) (p - 1);
 #if REDSET_HIP_TEST_KNOBS
   /* test builds: REDSET_HIP_TEST_XOR_DECODE=gather|chain forces one (A/B runs, tests) */
   const char* v = getenv("REDSET_HIP_TEST_XOR_DECODE");

@@ -172,7 +172,8 @@ ASAN_DRIVER = os.path.join(ROOT, "tests", "asan", "build", "rank_test")
 
 @pytest.mark.parametrize("scheme,p,e,lost,buf,maxsize", [("rs", 6, 2, [1, 4], 65536, 200_000),
                                                           ("rs", 5, 2, [0, 3], 65536, 20_000_000),
-                                                          ("xor", 4, 1, [2], 50000, 200_000)])
+                                                          ("xor", 4, 1, [2], 50000, 200_000),
+                                                          ("xor", 8, 1, [5], 2048, 200_000)])  # the chain
 def test_host_path_under_asan(stub, oracle, tmp_path, scheme, p, e, lost, buf, maxsize):
     """The same host path with the backends' host code built under
     AddressSanitizer (tests/asan, as tests/test_asan_host.py builds it):

@@ -185,7 +185,13 @@ def test_host_path_under_asan(stub, oracle, tmp_path, scheme, p, e, lost, buf, m
     assert res.returncode == 0, res.stdout + res.stderr
     env = {"_DRIVER": ASAN_DRIVER, "RANK_TEST_REPEAT": "2",
            "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=0:exitcode=86"}
-    _round_trip(oracle, str(tmp_path), scheme, p, e, lost, buf, 7 + p, maxsize, env=env)
+    _, reb, chunk = _round_trip(oracle, str(tmp_path), scheme, p, e, lost, buf, 7 + p, maxsize, env=env)
+    if scheme == "xor":
+        # the product's order rule (rank_mpi.c xor_decode_host): the chain for
+        # p >= 6 with >= 4 slices per hop, else the gather
+        chain = p >= 6 and -(-chunk // buf) >= 4 * (p - 1)
+        got = _stats(reb.stdout)["recv_bytes"][0]
+        assert got == (p if chain else (p - 1) * p) * chunk, (chain, got, chunk)
 
 
 TWIN_DIR = os.path.join(ROOT, "redset_amd", "lib_test")

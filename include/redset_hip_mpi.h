@@ -16,9 +16,13 @@
  *                                     (src/redset_reedsolomon.c:295, :588)
  *   redset_mpi_buf_size            -> buf_size (0 = 1 MiB, src/redset.c:45)
  * The message pattern of every MPI exchange is the reference's (RS encode
- * ring :329-363, RS decode ring + gather :646-733); XOR uses one all-to-all
- * per slice for encode and a gather to the root for decode (same bytes as
- * the reference's pipelined rings). All arithmetic runs on the GPU.
+ * ring :329-363, RS decode ring + gather :646-733), each cell sent straight
+ * to the member that combines it; the RS backends size their own slices from
+ * buf_size (rank_mpi.c slice_bytes). XOR uses one all-to-all per slice for
+ * encode, and for decode a gather to the root (small sets, short chunks) or
+ * the reference's pipelined chain through the survivors (src/redset_xor.c:
+ * 466-524, a slice of every stripe per message). All arithmetic runs on the
+ * GPU.
  * Collective over comm; returns REDSET_SUCCESS / REDSET_FAILURE; I/O errors
  * fail the call but the collective loop continues, as in the reference.
  */
@@ -50,21 +54,25 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
 int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
                                int fd_chunk, size_t chunk_size, size_t buf_size);
 
-/* The exchange of the multi-rank rebuild (the two decode backends above).
+/* The exchange of the four backends above (decode and, round 4, encode).
  * REDSET_HIP_EXCHANGE_AUTO (the default): when the members of `comm` are on
  * one node and each owns a distinct GPU (PCI bus id) and librccl loads on
- * every member, the decode runs as the sharded plan over RCCL / xGMI: every
- * member reads the cells the decode needs into HBM, the plan gathers column
- * slices of them onto every member's GPU, runs gf_mac on each slice and
- * returns the rebuilt slices to the lost members (replacing the decode ring
- * and gather, src/redset_reedsolomon.c:646-733, and the XOR reduce to the
- * root, src/redset_xor.c:466-524); otherwise the host-MPI path above. The
+ * every member, the call runs as the sharded plan over RCCL / xGMI: every
+ * member reads the cells the call needs into HBM, the plan gathers column
+ * slices of them onto every member's GPU, runs gf_mac (or the XOR) on each
+ * slice and returns the results to their members -- the rebuilt slices to
+ * the lost members (replacing the decode ring and gather,
+ * src/redset_reedsolomon.c:646-733, and the XOR reduce to the root,
+ * src/redset_xor.c:466-524), the parity slices to their holders (replacing
+ * the encode rings, :329-377, src/redset_xor.c:251-285); otherwise the
+ * host-MPI paths above. After a local device error a member still takes
+ * part in the exchange it is in, so no member waits forever. The
  * choice is made once per communicator (cached on it as an MPI attribute,
  * with the RCCL communicator, freed with it). _HOST_MPI and _SHARDED_RCCL
  * force a path; _SHARDED_MPI runs the sharded plan over the MPI transport
  * with device buffers (members may share a GPU). Process-wide; every member
- * of a set must pass the same mode (the decode checks and fails otherwise).
- * The exchange a decode used on this thread: redset_hip_rank_last_exchange. */
+ * of a set must pass the same mode (every call checks and fails otherwise).
+ * The exchange the last call used on this thread: redset_hip_rank_last_exchange. */
 enum {
   REDSET_HIP_EXCHANGE_AUTO = 0,
   REDSET_HIP_EXCHANGE_HOST_MPI = 1,

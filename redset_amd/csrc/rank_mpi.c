@@ -412,7 +412,9 @@ static int rs_encode_impl(const redset_hip_rs* rs, MPI_Comm comm, const redset_h
   const int d = p - e;
   const size_t buf = buf_size ? buf_size : DEFAULT_BUF;
   if (buf > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", buf); /* same on every rank */
-  const size_t B = slice_bytes(buf, chunk_size, (size_t) 3 * e);
+  /* the cells of the budget: the two parity buffers (the ring windows are
+   * bounded by MAX_STAGE below) */
+  const size_t B = slice_bytes(buf, chunk_size, (size_t) 2 * e);
   /* ring steps staged per window: the d*e slices of a slice's whole ring
    * would need d*e*B of pinned and device memory (O(p*e)); windows of G steps
    * bound each staging buffer to MAX_STAGE, the reference's own scratch being

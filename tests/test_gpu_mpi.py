@@ -449,3 +449,38 @@ def test_mpi_xor_decode_orders(oracle, tmp_path, order, p, lost, buf):
         assert os.path.getsize(path) == size
         assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
     assert np.array_equal(np.fromfile(reds[lost], dtype=np.uint8)[header[lost]:], want)
+
+
+@pytest.mark.parametrize("exchange", ["auto", "sharded-mpi"])
+def test_mpi_rs_slices_larger_than_the_buffer(oracle, tmp_path, exchange):
+    """~20 MB chunks with a 64 KiB buffer: the RS backends move slices of
+    chunk/16 (rank_mpi.c slice_bytes) and the encode stages whole ring
+    windows, on the GPU; parity against the oracle, rebuilt files by CRC32."""
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    tmp = str(tmp_path)
+    p, e, lost, buf = 6, 2, [0, 3], 65536
+    d = p - e
+    rng = np.random.default_rng(4242)
+    files, chunk = _setup(tmp, p, d, rng, 30_000_000)
+    header = [4096] * p
+    reds = [os.path.join(tmp, f"r{r}.rs.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, header, reds)
+    crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for r in lost for path, _ in files[r]}
+    res = _mpirun(p, ["rs", "encode", e, tmp, buf], env=_exchange_env(exchange))
+    assert res.returncode == 0, res.stdout + res.stderr
+    lofi = [_logical(fl, d * chunk) for fl in files]
+    want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+    oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+    for r in range(p):
+        assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[4096:], want[r]), r
+    for r in lost:
+        for path, _ in files[r]:
+            os.unlink(path)
+        os.unlink(reds[r])
+    res = _mpirun(p, ["rs", "rebuild", e, tmp, buf] + lost, env=_exchange_env(exchange))
+    assert res.returncode == 0, res.stdout + res.stderr
+    for r in lost:
+        for path, size in files[r]:
+            assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
+        assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[4096:], want[r]), r

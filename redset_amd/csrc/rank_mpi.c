@@ -1543,11 +1543,8 @@ static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream
     T->stage = NULL;
     T->stage_len = 0;
     T->stage_pinned = hipHostMalloc((void**) &T->stage, need, hipHostMallocDefault) == hipSuccess;
-    if (!T->stage_pinned) {
-      /* pageable memory still carries the messages */
-      T->stage = malloc(need);
-      rc = fail("mpi transport: hipHostMalloc(%zu) failed", need);
-    }
+    /* pageable memory carries the messages as well (its copies are slower) */
+    if (!T->stage_pinned) T->stage = malloc(need);
     if (!T->stage) return fail("mpi transport: out of host memory (%zu)", need);
     T->stage_len = need;
   }

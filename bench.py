@@ -9,7 +9,7 @@ members {1, 2} from the survivors. Both passes run the gf_mac HIP kernel.
 (10^9 B). Algorithmic bytes per stripe: encode (d + e)*C, rebuild (d + m)*C
 (SURVEY.md §8d).
 
-N>1 (torchrun, one process per GPU, RCCL): weak scaling. Redundancy sets are
+N>1 (one process per GPU, RCCL): weak scaling. Redundancy sets are
 independent objects, so the timed step shards them across ranks with no
 data-path collective: every GPU encodes + rebuilds its own set exactly as at
 N=1, and `value` = all ranks' algorithmic bytes / the max-over-ranks step
@@ -19,12 +19,21 @@ after it as a second timed leg and reported under "sharded": N sets whose
 members are spread round-robin over the GPUs, erased members rebuilt
 column-sharded over all GPUs after an RCCL P2P gather of the decode inputs'
 slices (redset_amd.dist), exchange inside the timing, result checked bit-exact.
+The sharded leg runs at N=1 too (world-1 RCCL transport: the gather and
+return are local copies), so configs[3]'s curve has its base point in every
+N=1 line; `sharded.value` is configs[3]'s scaling number at every N.
+
+Launch: under torchrun (RANK / WORLD_SIZE set) every process is one rank.
+`--gpus N > 1` without torchrun starts the N ranks itself, as a torchrun child
+process, before this process touches the GPU, and relays rank 0's line.
 
 Prints ONE JSON line on rank 0.
 """
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import threading
 import time
@@ -55,7 +64,10 @@ def parse():
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration (RS; XOR gets half)")
     ap.add_argument("--cpu-chunk-mib", type=float, default=0.0,
                     help="chunk of the CPU baseline's set (0: the GPU workload's own chunk)")
-    ap.add_argument("--sharded", type=int, default=1, help="N>1: also time the RCCL sharded-rebuild leg")
+    ap.add_argument("--sharded", type=int, default=1,
+                    help="also time the RCCL sharded-rebuild leg (configs[3]; at N=1 over the world-1 transport)")
+    ap.add_argument("--launch-timeout", type=float, default=1500.0,
+                    help="self-launched N>1 runs: seconds before the rank processes are stopped")
     ap.add_argument("--sharded-timeout", type=float, default=150.0,
                     help="seconds the sharded leg may take before the main line is printed without it")
     ap.add_argument("--xor", type=int, default=1, help="also time the XOR set of configs[1] (rank 0)")
@@ -397,34 +409,44 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     of every decode input over RCCL, gf_mac, return the rebuilt slices to
     their hosts. Parity comes from one untimed sharded encode beforehand.
     After timing every GPU checks that its lost members' slabs are back bit
-    for bit (min over ranks)."""
+    for bit (min over ranks). At world 1 (no process group) the transport is
+    RCCL over a one-rank communicator: gather and return are local copies
+    and the step is configs[3]'s N=1 point."""
     import torch
     import torch.distributed as dist
+
+    import redset_amd
     from redset_amd import dist as rdist
+
+    dist_on = world > 1
+    dev = "cuda" if (not dist_on or dist.get_backend() == "nccl") else "cpu"
+
+    def reduce(x, op, dtype):
+        t = torch.tensor([x], dtype=dtype, device=dev)
+        if dist_on:
+            dist.all_reduce(t, op=op)
+        return t.item()
 
     runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank)
     runner.encode()
     snap = runner.lost_snapshot()
     runner.erase()
-    s_elapsed = timed(lambda i: runner.rebuild(), args.steps, args.warmup, True, before=runner.reset_timing)
+    s_elapsed = timed(lambda i: runner.rebuild(), args.steps, args.warmup, dist_on, before=runner.reset_timing)
     s_step = s_elapsed / args.steps
-    ok = torch.tensor([1 if runner.matches(snap) else 0], dtype=torch.int32,
-                      device="cuda" if dist.get_backend() == "nccl" else "cpu")
-    dist.all_reduce(ok, op=dist.ReduceOp.MIN)
+    torch.cuda.synchronize()
+    hangs = redset_amd.hang_faults()
+    ok = reduce(1 if runner.matches(snap) and hangs == 0 else 0, dist.ReduceOp.MIN, torch.int32)
     value = world * runner.algorithmic_bytes("rebuild") / s_step / 1e9
     # bytes each GPU sends over the fabric per rebuild (C planner's count),
     # mean and max over the ranks
-    dev = "cuda" if dist.get_backend() == "nccl" else "cpu"
-    sent = torch.tensor([float(runner.exchanged_bytes("rebuild"))], dtype=torch.float64, device=dev)
-    sent_max = sent.clone()
-    dist.all_reduce(sent, op=dist.ReduceOp.SUM)
-    dist.all_reduce(sent_max, op=dist.ReduceOp.MAX)
-    sent_mean, sent_max = sent.item() / world, sent_max.item()
+    sent_mine = float(runner.exchanged_bytes("rebuild"))
+    sent_mean = reduce(sent_mine, dist.ReduceOp.SUM, torch.float64) / world
+    sent_max = reduce(sent_mine, dist.ReduceOp.MAX, torch.float64)
     # untimed diagnostic: the same rebuild with its three phases one after
     # another (no overlap across sets), timed apart by events on rank 0
     pipelined_event_ms = runner.phase_ms().get("rebuild_start->done")
     runner.phased = True
-    timed(lambda i: runner.rebuild(), 3, 1, True, before=runner.reset_timing)
+    timed(lambda i: runner.rebuild(), 3, 1, dist_on, before=runner.reset_timing)
     phases = runner.phase_ms()
     compute_ms = phases.get("rebuild_gathered->computed")
     # The step's roofline is the fabric, not HBM: every GPU sends its
@@ -433,25 +455,40 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     # xGMI mesh: one link per peer pair, world - 1 links usable per GPU).
     link_peak = (world - 1) * XGMI_LINK_GBPS
     fabric_gbps = sent_mean / s_step / 1e9
+    local_bytes = int(runner.info("rebuild")["local_bytes"])
     out = {
-        "workload": (f"{world} sets of p={p} (RS({p - e}+{e}), chunk {chunk >> 20} MiB), members round-robin over "
+        "workload": (f"{world} sets of p={p} (RS({p - e}+{e}), chunk {chunk / MIB:g} MiB), members round-robin over "
                      f"{world} GPUs; rebuild of members {lost} of every set, column-sharded (BASELINE.json configs[3])"),
         "value": round(value, 2),
         "unit": "GB/s",
+        # north_star: the sharded rebuild "as absolute GB/s and as fraction of HBM peak"
+        "frac_of_hbm": round(value / (world * HBM_PEAK_GBPS), 4),
+        "hbm_peak_GBps": world * HBM_PEAK_GBPS,
         "ms_per_step": round(s_step * 1e3, 4),
-        "bit_exact": bool(ok.item()),
+        "bit_exact": bool(ok),
+        "transport": type(runner._transport).__name__ + ("" if dist_on else " (world 1: local copies)"),
         "schedule": "sets pipelined: set k+1's gather overlaps set k's gf_mac (redset_hip_sharded_execute)",
         "pipelined_event_ms_rank0": pipelined_event_ms,
         "roofline": {
             "bound": "xgmi",
-            "achieved": round(fabric_gbps, 2) if world > 1 else None,
-            "peak": link_peak if world > 1 else None,
+            "achieved": round(fabric_gbps, 2),
+            "peak": link_peak,
             "unit": "GB/s per GPU (bytes sent over the fabric / step time)",
-            "frac": round(fabric_gbps / link_peak, 4) if world > 1 else None,
+            "frac": round(fabric_gbps / link_peak, 4),
             "bytes_sent_per_gpu_per_step": {"mean": int(sent_mean), "max": int(sent_max)},
             "peak_source": (f"{XGMI_LINK_GBPS:g} GB/s per xGMI link and direction x (world - 1) links: one link per "
                             "GPU pair of the node's fully connected mesh, 7 per GPU at 8 GPUs (SURVEY.md §5; "
                             "MI355X platform figure, not measured here)"),
+        } if dist_on else {
+            # world 1: nothing crosses the fabric; the step is HBM-bound --
+            # the gather's and return's local copies (read + write) plus the
+            # gf_mac's own algorithmic bytes
+            "bound": "hbm",
+            "achieved": round((2 * local_bytes + runner.algorithmic_bytes("rebuild")) / s_step / 1e9, 1),
+            "peak": HBM_PEAK_GBPS,
+            "unit": "GB/s (HBM bytes of copies + gf_mac / step time)",
+            "frac": round((2 * local_bytes + runner.algorithmic_bytes("rebuild")) / s_step / 1e9 / HBM_PEAK_GBPS, 4),
+            "local_copy_bytes_per_step": local_bytes,
         },
         # HBM is the bound of the compute phase alone (phased diagnostic)
         "compute_hbm": {
@@ -497,17 +534,69 @@ def sharded_expired(result, rank, limit):
         os._exit(WATCHDOG_EXIT)
 
 
+def _free_port():
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def relay(lines, out=sys.stdout, err=sys.stderr):
+    """Pass the rank processes' output on: the first JSON line carrying
+    "metric" (rank 0's result) to `out`, everything else to `err` as it comes
+    (so a long run shows progress). Returns whether the line was seen."""
+    seen = False
+    for ln in lines:
+        s = ln.strip()
+        if not seen and s.startswith("{"):
+            try:
+                if "metric" in json.loads(s):
+                    print(s, file=out, flush=True)
+                    seen = True
+                    continue
+            except ValueError:
+                pass
+        print(ln.rstrip("\n"), file=err, flush=True)
+    return seen
+
+
+def self_launch(argv, n, timeout, cmd=None):
+    """`--gpus n > 1` without torchrun: start the n ranks as ONE child process
+    (torch.distributed.run, rendezvous on 127.0.0.1) before this process makes
+    any GPU call -- it never initialises the GPU and never execs -- and relay
+    rank 0's line. The child's exit status is returned; a child still running
+    after `timeout` seconds is stopped (its whole process group) and counts as
+    failed."""
+    if cmd is None:
+        cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+               "--master-addr", "127.0.0.1", f"--master-port={_free_port()}",
+               os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, PYTHONUNBUFFERED="1")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, stderr=None, text=True, env=env, start_new_session=True)
+    killer = threading.Timer(timeout, lambda: os.killpg(proc.pid, 9))
+    killer.daemon = True
+    killer.start()
+    try:
+        seen = relay(proc.stdout)
+        rc = proc.wait()
+    finally:
+        killer.cancel()
+    if not seen:
+        print(json.dumps({"error": f"the {n} rank processes printed no result line (exit status {rc})"}), flush=True)
+    return rc if rc != 0 or seen else 1
+
+
 def main():
     args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world == 1 and args.gpus > 1 and "RANK" not in os.environ:
+        sys.exit(self_launch(sys.argv[1:], args.gpus, args.launch_timeout))
     import torch
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        if world == 1 and args.gpus > 1:
-            print(json.dumps({"error": f"--gpus {args.gpus} needs torchrun with {args.gpus} processes"}))
-            sys.exit(2)
+        print(json.dumps({"error": f"--gpus {args.gpus} but WORLD_SIZE={world}"}))
+        sys.exit(2)
     dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)
     dist_on = world > 1
@@ -560,7 +649,10 @@ def main():
     rt_ok = round_trip(lay, enc_plan, reb_plan, lost, stream)
     # every launch so far (timed steps included) completed its loader-ring handshakes
     ring_faults = redset_amd.ring_faults()
-    rt_ok = rt_ok and ring_faults == 0
+    # no kernel wait without a fallback gave up (include/redset_hip.h
+    # redset_hip_hang_faults): a nonzero count means wrong bytes somewhere
+    hang_faults = redset_amd.hang_faults()
+    rt_ok = rt_ok and ring_faults == 0 and hang_faults == 0
     if dist_on:
         flag = torch.tensor([int(rt_ok)], dtype=torch.int32, device="cuda" if args.dist_backend == "nccl" else "cpu")
         dist.all_reduce(flag, op=dist.ReduceOp.MIN)
@@ -591,6 +683,11 @@ def main():
             "sets": world,
             "bytes_per_step_per_gpu": bytes_per_step,
             "parallelism": "single GPU" if world == 1 else f"{world} independent sets, one per GPU (no collective)",
+            # which number is which: `value` is the independent-sets step
+            # (configs[2] + configs[3] on each GPU), comparable from N=1 to
+            # N=8; configs[3]'s multi-GPU scaling curve is sharded.value
+            "scaling_value": ("sharded.value: configs[3]'s column-sharded rebuild over RCCL/xGMI, "
+                              "with sharded.frac_of_hbm" if args.sharded else None),
         },
     }
     step_ms = sorted(ev[k][0].elapsed_time(ev[k][2]) for k in range(args.steps))
@@ -639,6 +736,7 @@ def main():
     }
     result["round_trip_bit_exact"] = rt_ok
     result["ring_faults"] = ring_faults
+    result["hang_faults"] = hang_faults
     result["box_reference"] = {
         "torch_copy_GBps": box_copy,
         "codec_vs_copy": round(achieved / box_copy, 4),
@@ -658,10 +756,11 @@ def main():
         watchdog = threading.Timer(args.sharded_timeout, sharded_expired, (result, rank, args.sharded_timeout))
         watchdog.daemon = True
         watchdog.start()
-    if dist_on and args.sharded:
-        # second leg: the multi-rank rebuild with its RCCL exchange. It must
-        # not cost the main line: a failure is reported in "sharded" (every
-        # rank runs the same collectives, so they fail alike).
+    if args.sharded:
+        # second leg: the multi-rank rebuild with its RCCL exchange (at N=1
+        # the world-1 transport). It must not cost the main line: a failure
+        # is reported in "sharded" (every rank runs the same collectives, so
+        # they fail alike).
         try:
             result["sharded"] = sharded_leg(args, p, e, chunk, lost, world, rank)
         except Exception as exc:  # noqa: BLE001 -- reported, not swallowed

@@ -320,6 +320,7 @@ typedef struct {
   unsigned long long gather_msg_min;
   unsigned long long return_msg_max;
   unsigned long long return_msg_min;
+  int gather_recv_messages, return_recv_messages; /* peer messages this process receives */
 } redset_hip_sharded_info;
 
 typedef struct redset_hip_sharded redset_hip_sharded;
@@ -373,17 +374,35 @@ int redset_hip_rccl_transport_create(const unsigned char id[128], int world, int
                                      redset_hip_rccl** handle);
 void redset_hip_rccl_transport_destroy(redset_hip_rccl* handle);
 
-/* Capped handshake spins of the kernels' loader-wave ring on the current
- * device since the last clearing read. A capped spin never costs
- * correctness: the waiting consumer (or, after a capped loader, every
- * consumer of the rest of the launch) loads its bytes straight from HBM, so
- * every call's outputs are right whatever this returns. A nonzero count in
- * the shipped build (cap 2^24 polls) means a ring stalled and ran slower --
- * a performance event worth reporting, not an error. It happened once in
- * development, from a since-fixed missing barrier (round 2). The count is
- * per device and process-wide, so concurrent callers share it.
- * Synchronises the device; `clear` resets the count. */
+/* The kernels count two kinds of capped waits, per device and process-wide
+ * (concurrent callers share the counts):
+ *
+ * Capped handshake SPINS of the loader-wave ring (redset_hip_ring_faults),
+ * since the last clearing read. A capped spin never costs correctness: the
+ * waiting consumer (or, after a capped loader, every consumer of the rest of
+ * the launch) loads its bytes straight from HBM. A nonzero count in the
+ * shipped build (cap 2^24 polls) means a ring stalled and ran slower -- a
+ * performance event worth reporting, not an error. It happened once in
+ * development, from a since-fixed missing barrier (round 2). Synchronises the
+ * device; `clear` resets the count. */
 int redset_hip_ring_faults(unsigned* count, int clear);
+
+/* Capped HANG waits (redset_hip_hang_faults): waits that end by construction
+ * and have no fallback -- the streamed and claimed kernels' table hand-over,
+ * claim records and end-of-sequence agreement. Their cap (2^26 polls) only
+ * keeps a bug from hanging the GPU; a capped one proceeds with another job's
+ * tables or drops rows, so THAT LAUNCH'S OUTPUTS ARE WRONG. The synchronous
+ * entry points that run kernels -- the streaming calls, the per-rank backends
+ * of redset_hip_mpi.h (host and sharded exchanges) and the offline rebuild
+ * tool -- read this count before and after their work and return
+ * REDSET_FAILURE when it moved, so they never report success with wrong
+ * bytes (a concurrent caller's hang on the same device fails them too). The
+ * asynchronous ones (redset_hip_plan_execute, redset_hip_sharded_execute,
+ * the stripe primitives) cannot: their caller reads this after its own sync.
+ * The read is ordered on `stream` after the work already there and waits
+ * for it; NULL reads on the library's own non-blocking stream, ordered after
+ * nothing (sync the work to be counted first). `clear` resets the count. */
+int redset_hip_hang_faults(void* stream, unsigned* count, int clear);
 
 /* 1 if this is the test twin library (built with REDSET_HIP_TEST_KNOBS: it
  * honours the environment knobs the test suite uses to force job orders,

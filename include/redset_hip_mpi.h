@@ -54,25 +54,26 @@ int redset_hip_xor_encode_rank(MPI_Comm comm, const redset_hip_io* lofi, const c
 int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lofi, const char* chunk_file,
                                int fd_chunk, size_t chunk_size, size_t buf_size);
 
-/* The exchange of the four backends above (decode and, round 4, encode).
- * REDSET_HIP_EXCHANGE_AUTO (the default): when the members of `comm` are on
- * one node and each owns a distinct GPU (PCI bus id) and librccl loads on
- * every member, the call runs as the sharded plan over RCCL / xGMI: every
- * member reads the cells the call needs into HBM, the plan gathers column
- * slices of them onto every member's GPU, runs gf_mac (or the XOR) on each
- * slice and returns the results to their members -- the rebuilt slices to
- * the lost members (replacing the decode ring and gather,
- * src/redset_reedsolomon.c:646-733, and the XOR reduce to the root,
- * src/redset_xor.c:466-524), the parity slices to their holders (replacing
- * the encode rings, :329-377, src/redset_xor.c:251-285); otherwise the
- * host-MPI paths above. After a local device error a member still takes
- * part in the exchange it is in, so no member waits forever. The
- * choice is made once per communicator (cached on it as an MPI attribute,
- * with the RCCL communicator, freed with it). _HOST_MPI and _SHARDED_RCCL
- * force a path; _SHARDED_MPI runs the sharded plan over the MPI transport
- * with device buffers (members may share a GPU). Process-wide; every member
- * of a set must pass the same mode (every call checks and fails otherwise).
- * The exchange the last call used on this thread: redset_hip_rank_last_exchange. */
+/* The exchange of the four backends above.
+ * REDSET_HIP_EXCHANGE_AUTO (the default): a DECODE whose members are on one
+ * node, each owning a distinct GPU (PCI bus id), with librccl loadable on
+ * every member, runs as the sharded plan over RCCL / xGMI: every member reads
+ * the cells the call needs into HBM, the plan gathers column slices of them
+ * onto every member's GPU, runs gf_mac (or the XOR) on each slice and returns
+ * the rebuilt slices to the lost members (replacing the decode ring and
+ * gather, src/redset_reedsolomon.c:646-733, and the XOR reduce to the root,
+ * src/redset_xor.c:466-524). Encodes, and decodes elsewhere, take the
+ * host-MPI paths above (north_star: RCCL only for the multi-rank rebuild).
+ * _HOST_MPI and _SHARDED_RCCL force a path for every call (the encodes too:
+ * the parity slices then return to their holders, replacing the encode
+ * rings, :329-377, src/redset_xor.c:251-285); _SHARDED_MPI runs the sharded
+ * plan over the MPI transport with device buffers (members may share a GPU).
+ * After a local device error a member still takes part in the exchange it
+ * is in, so no member waits forever. The RCCL decision is made once per
+ * communicator (cached on it as an MPI attribute, with the RCCL
+ * communicator, freed with it). Process-wide; every member of a set must
+ * pass the same mode (every call checks and fails otherwise). The exchange
+ * the last call used on this thread: redset_hip_rank_last_exchange. */
 enum {
   REDSET_HIP_EXCHANGE_AUTO = 0,
   REDSET_HIP_EXCHANGE_HOST_MPI = 1,
@@ -86,20 +87,40 @@ int redset_hip_rank_last_exchange(void);
  * (one member's view): bytes read from the logical file and the redundancy
  * file, sent and received over MPI (or, sharded, over the exchange's
  * transport), copied to and from the GPU, written; and the seconds its host
- * thread spent blocked in file I/O, in MPI waits and waiting for the GPU
- * (copies, kernels, a sharded exchange) -- at most the whole call. */
+ * thread spent blocked, in disjoint classes whose sum is at most the call:
+ *   read / write_seconds   file I/O
+ *   mpi_seconds            MPI waits: the exchanges' Waitall (the MPI
+ *                          transport's too) and the per-window agreements
+ *   gpu_seconds            waiting for the GPU's copies and kernels (event
+ *                          and stream waits; a stream-ordered RCCL exchange
+ *                          is waited for here)
+ *   stage_seconds          the MPI transport's staging of device messages
+ *                          through pinned memory (D2H / H2D copies, waited)
+ *   copy_seconds           enqueueing the sharded windows' H2D / D2H copies
+ *   plan_seconds           planning the sharded exchanges
+ * exchange_seconds is the host time inside redset_hip_sharded_execute (the
+ * sharded calls' exchanges and kernels; it contains their mpi, gpu and stage
+ * time and is not one of the classes). */
 typedef struct {
   double seconds;
   double read_seconds, mpi_seconds, gpu_seconds, write_seconds;
   unsigned long long read_bytes, sent_bytes, recv_bytes, h2d_bytes, d2h_bytes, write_bytes;
+  double stage_seconds, copy_seconds, plan_seconds, exchange_seconds;
 } redset_hip_rank_stats;
 int redset_hip_rank_last_stats(redset_hip_rank_stats* out);
 
-/* The backends above keep a successful call's pinned host buffers, device
- * buffers and stream for the next call (at most 256 MiB pinned, 1 GiB of
- * device memory); REDSET_HIP_SCRATCH_CACHE=0 allocates and frees per call
- * instead, as the reference does (src/redset_reedsolomon.c:298-302, :397-399).
- * This frees the cache (and redset_hip_release_scratch's), e.g. from
+/* Page-locked host memory one call takes per member (and about as much
+ * device memory): the RS host paths at most 256 MiB of slice buffers (encode
+ * (2e+1)*G + 2e slices, decode 4p + 2*missing; rank_mpi.c cuts the slice to
+ * fit: RS(8+3) at 64 MiB chunks takes 248 MiB to encode); the XOR host
+ * paths a few buffers of buf_size; the sharded exchanges two window images
+ * of 96 MiB, plus, over the MPI transport (_SHARDED_MPI), a staging buffer of
+ * one exchange's bytes sent and received (up to ~2 x 96 MiB).
+ * The backends keep a successful call's pinned host buffers, device buffers
+ * and stream for the next call (at most 256 MiB pinned, 1 GiB of device
+ * memory); REDSET_HIP_SCRATCH_CACHE=0 allocates and frees per call instead,
+ * as the reference does (src/redset_reedsolomon.c:298-302, :397-399). This
+ * frees the cache (and redset_hip_release_scratch's), e.g. from
  * redset_finalize. */
 void redset_hip_rank_scratch_release(void);
 
@@ -117,6 +138,15 @@ void redset_hip_rank_scratch_release(void);
 typedef struct redset_hip_mpi_transport redset_hip_mpi_transport;
 int redset_hip_mpi_transport_create(MPI_Comm comm, int device_buffers, redset_hip_transport* out,
                                     redset_hip_mpi_transport** handle);
+/* Size the transport's staging (device mode) and MPI request buffers for
+ * exchanges of up to `bytes` of messages to and from other processes and
+ * `messages` such messages (redset_hip_sharded_info: bytes sent + received,
+ * messages sent + received, of the largest exchange). Local; agree on the
+ * result before the first exchange. An exchange that finds its buffers too
+ * small allocates them itself, and a failure there returns before any
+ * message is posted -- the peers then wait in that exchange -- so callers
+ * that can fail must reserve first (the per-rank backends do). */
+int redset_hip_mpi_transport_reserve(redset_hip_mpi_transport* handle, size_t bytes, size_t messages);
 void redset_hip_mpi_transport_destroy(redset_hip_mpi_transport* handle);
 
 #ifdef __cplusplus

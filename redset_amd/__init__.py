@@ -16,6 +16,7 @@ from .codec import (  # noqa: F401
     gf_combine,
     cell_stride,
     ring_faults,
+    hang_faults,
     xor_combine,
     xor_plan_encode,
     xor_plan_rebuild,

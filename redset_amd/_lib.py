@@ -44,6 +44,7 @@ EXPORTED_SYMBOLS = (
     "redset_hip_xor_combine",
     "redset_hip_rs_decode_matrix",
     "redset_hip_ring_faults",
+    "redset_hip_hang_faults",
     "redset_hip_test_build",
     "redset_hip_last_error",
     "redset_hip_record_error",
@@ -172,6 +173,8 @@ class ShardedInfo(ctypes.Structure):
         ("gather_msg_min", c_ulonglong),
         ("return_msg_max", c_ulonglong),
         ("return_msg_min", c_ulonglong),
+        ("gather_recv_messages", c_int),
+        ("return_recv_messages", c_int),
     ]
 
     def as_dict(self):
@@ -232,6 +235,7 @@ _SIGNATURES = {
     "redset_hip_rccl_transport_create": (c_int, [POINTER(c_ubyte), c_int, c_int, POINTER(Transport), POINTER(c_void_p)]),
     "redset_hip_rccl_transport_destroy": (None, [c_void_p]),
     "redset_hip_ring_faults": (c_int, [POINTER(c_uint), c_int]),
+    "redset_hip_hang_faults": (c_int, [c_void_p, POINTER(c_uint), c_int]),
     "redset_hip_test_build": (c_int, []),
     "redset_hip_last_error": (c_char_p, []),
     "redset_hip_record_error": (c_int, [c_char_p]),

@@ -274,3 +274,17 @@ def ring_faults(clear: bool = True) -> int:
     n = c_uint(0)
     _lib.check(_lib.load().redset_hip_ring_faults(ctypes.byref(n), int(clear)), "ring_faults")
     return int(n.value)
+
+
+def hang_faults(clear: bool = True, stream=None) -> int:
+    """Capped HANG waits on the current device since the last clearing read
+    (include/redset_hip.h redset_hip_hang_faults): waits with no fallback
+    that gave up, so some launch's outputs are wrong. 0 on every healthy
+    run. Read in order on `stream` (default: the library's own stream, after
+    nothing -- synchronise the work to be counted first)."""
+    from ctypes import c_uint
+
+    n = c_uint(0)
+    h = None if stream is None else _stream_handle(stream)
+    _lib.check(_lib.load().redset_hip_hang_faults(h, ctypes.byref(n), int(clear)), "hang_faults")
+    return int(n.value)

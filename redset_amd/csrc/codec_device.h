@@ -220,8 +220,9 @@ struct XorAcc {
 // slot); a loader whose FREE wait caps stops streaming without touching the
 // busy slot and raises the block's BYPASS word, after which every item it
 // has not published is loaded directly by its consumer. Each capped spin
-// adds 1 to the launch's fault word (redset_hip_ring_faults()): a
-// performance event, not an error. Capped spins did happen once, from a
+// adds 1 to the launch's first fault word (redset_hip_ring_faults()): a
+// performance event, not an error. (Waits with no fallback count in the
+// second word instead, see kRingHangCap.) Capped spins did happen once, from a
 // missing barrier between the jobs of an in-kernel job loop (round 2,
 // profiles/r02s62_gpu_tests_ring_fault.log, fixed at the top of ring_sweep);
 // the test twin library runs the suite with a 4-poll cap, which drives both
@@ -273,10 +274,32 @@ constexpr unsigned kRingSpinCap = 1u << 24;
 #define RING_SPIN_CAP(L) kRingSpinCap
 #endif
 // Waits that end by construction and have no fallback (the streamed kernels'
-// table hand-over and a position's claim): their cap is only insurance
-// against a hang from a bug, counted like a capped spin, and independent of
-// the test cap above (a capped table wait would use another job's tables).
+// table hand-over, the claimed kernel's claim records and its loader's wait
+// for the claimer): their cap is only insurance against a hang from a bug.
+// A capped one is NOT a performance event -- the wait proceeds with another
+// job's tables or drops positions, so the launch's outputs are wrong -- and
+// it counts in the launch's SECOND fault word (L.fault[1], the hang word;
+// redset_hip_hang_faults). Every product entry point that runs kernels reads
+// that word after its last sync and fails the call when it moved. The test
+// twin takes this cap from the launch too (GfLaunch::hang_cap,
+// REDSET_HIP_TEST_HANG_CAP), independent of the spin cap, so the suite can
+// make it fire and check that the call fails.
 constexpr unsigned kRingHangCap = 1u << 26;
+#if REDSET_HIP_TEST_KNOBS
+#define RING_HANG_CAP(L) ((L).hang_cap)
+#else
+#define RING_HANG_CAP(L) kRingHangCap
+#endif
+#define RING_HANG_FAULT(L) atomicAdd((L).fault + 1, 1u)
+// Test builds: the loader sleeps before it publishes a job's tables
+// (REDSET_HIP_TEST_TABLE_DELAY rounds of s_sleep 127), so consumers reach the
+// next job first and wait on the table hand-over.
+#if REDSET_HIP_TEST_KNOBS
+#define RING_TABLE_DELAY(L) \
+  for (unsigned d_ = 0; d_ < (L).table_delay; ++d_) __builtin_amdgcn_s_sleep(127)
+#else
+#define RING_TABLE_DELAY(L) (void) 0
+#endif
 // Inputs a ring consumer holds in VGPRs at once; wider stripes are combined in
 // two chunks (ring_sweep).
 constexpr int kRingChunk = 8;
@@ -668,13 +691,14 @@ __device__ __forceinline__ void gf_mac_stream(const GfLaunch& L) {
         ring_wait_vm<0>();
         while (pub < g) publish();
         // always ends (see above); the cap only keeps a bug from hanging the
-        // GPU -- a capped wait is counted and every test checks the count
+        // GPU -- a capped wait goes to the hang word and fails the call
         unsigned spins = 0;
-        while (!past((j - 1) * K) && ++spins < kRingHangCap) __builtin_amdgcn_s_sleep(1);
-        if (spins >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+        while (!past((j - 1) * K) && ++spins < RING_HANG_CAP(L)) __builtin_amdgcn_s_sleep(1);
+        if (spins >= RING_HANG_CAP(L) && lane == 0 && L.fault) RING_HANG_FAULT(L);
       }
       build_tables_wave<NIN, NOUT>(lds, (j & 1) * kTab, jobs + j, lane);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      RING_TABLE_DELAY(L);
       if (lane == 0) ring_flag_st(&tab_job, j);
     };
     const uint8_t* in[NIN];
@@ -734,8 +758,8 @@ __device__ __forceinline__ void gf_mac_stream(const GfLaunch& L) {
     if (static_cast<int>(job) != cur) {
       cur = static_cast<int>(job);
       unsigned spins = 0;  // always ends; capped as the loader's wait above
-      while (ring_flag_ld(&tab_job) < job && ++spins < kRingHangCap) __builtin_amdgcn_s_sleep(kRingSleep);
-      if (spins >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+      while (ring_flag_ld(&tab_job) < job && ++spins < RING_HANG_CAP(L)) __builtin_amdgcn_s_sleep(kRingSleep);
+      if (spins >= RING_HANG_CAP(L) && lane == 0 && L.fault) RING_HANG_FAULT(L);
 #pragma unroll
       for (int i = 0; i < NIN; ++i) in[i] = (g_cu4*) (jobs[job].in[i]);
 #pragma unroll
@@ -1003,12 +1027,13 @@ __device__ __forceinline__ void claimed_sweep(const typename Pol::Launch& L) {
             ring_wait_vm<0>();
             while (pub < p) publish();
             unsigned spins = 0;
-            while (!past(T) && ++spins < kRingHangCap) __builtin_amdgcn_s_sleep(1);
-            if (spins >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+            while (!past(T) && ++spins < RING_HANG_CAP(L)) __builtin_amdgcn_s_sleep(1);
+            if (spins >= RING_HANG_CAP(L) && lane == 0 && L.fault) RING_HANG_FAULT(L);
           }
           if constexpr (Pol::kTables) {
             Pol::next_tables(lds, jobs + job, job, lane);
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            RING_TABLE_DELAY(L);
             if (lane == 0) ring_flag_st(&tab_job, job);
           }
 #pragma unroll
@@ -1059,8 +1084,8 @@ __device__ __forceinline__ void claimed_sweep(const typename Pol::Launch& L) {
       // last one (it stops promptly after BYPASS; hang cap only)
       if (stop) {
         unsigned spins = 0;
-        while (ring_flag_ld(&claimer_done) == 0u && ++spins < kRingHangCap) __builtin_amdgcn_s_sleep(1);
-        if (spins >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+        while (ring_flag_ld(&claimer_done) == 0u && ++spins < RING_HANG_CAP(L)) __builtin_amdgcn_s_sleep(1);
+        if (spins >= RING_HANG_CAP(L) && lane == 0 && L.fault) RING_HANG_FAULT(L);
       }
       if (lane == 0) {
         const unsigned nc = ring_flag_ld(&nclaimed);
@@ -1138,9 +1163,9 @@ __device__ __forceinline__ void claimed_sweep(const typename Pol::Launch& L) {
         // Nothing else keeps the claim back, so the wait ends (hang cap only)
         unsigned s3 = 0;
         while (ring_flag_ld(&nclaimed) <= p / B && ring_flag_ld(&claim_end) > p / B &&
-               ring_flag_ld(&claimer_done) == 0u && ++s3 < kRingHangCap)
+               ring_flag_ld(&claimer_done) == 0u && ++s3 < RING_HANG_CAP(L))
           __builtin_amdgcn_s_sleep(1);
-        if (s3 >= kRingHangCap && lane == 0 && L.fault) atomicAdd(L.fault, 1u);
+        if (s3 >= RING_HANG_CAP(L) && lane == 0 && L.fault) RING_HANG_FAULT(L);
         if (ring_flag_ld(&nclaimed) <= p / B) break;
         u = ring_flag_ld(&bbase[(p / B) % NB]) + p % B;
       }

@@ -67,10 +67,13 @@ struct GfLaunch {
   int group;                // kJobsInLaunches: jobs per launch, side by side (0 = 1);
                             // kJobsStreamed / kJobsClaimed: jobs per launch, in turn (0 = all)
   size_t nbytes;            // bytes per cell
-  unsigned* fault;          // set by the launcher: counts capped ring spins (codec_device.h)
+  unsigned* fault;          // set by the launcher: two device words, [0] capped ring spins (a direct-load
+                            // fallback ran), [1] capped hang waits (outputs wrong; codec_device.h kRingHangCap)
   unsigned* claim;          // kJobsClaimed: kClaimWords device words (plan; zeroed per launch)
   unsigned spin_cap;        // set by the launcher; read by test builds only (codec_device.h kRingSpinCap)
   unsigned claim_delay;     // test builds: s_sleep rounds the claimer waits between claiming and recording
+  unsigned hang_cap;        // test builds: polls before a wait with no fallback gives up (kRingHangCap)
+  unsigned table_delay;     // test builds: s_sleep rounds before a loader publishes a job's tables
 };
 
 // XOR of `nin` inputs into one output (the XOR scheme's parity / rebuild).
@@ -94,6 +97,8 @@ struct XorLaunch {
   unsigned* claim;          // kJobsClaimed (see GfLaunch)
   unsigned spin_cap;        // (see GfLaunch)
   unsigned claim_delay;     // (see GfLaunch)
+  unsigned hang_cap;        // (see GfLaunch)
+  unsigned table_delay;     // (see GfLaunch)
 };
 
 // launchers (codec_kernels.hip); return hipError_t as int
@@ -105,9 +110,15 @@ int launch_xor_single(const XorLaunch& L, const XorJob& J, void* stream);
 // device properties used to size grids
 int device_cu_count();
 // the current device's count of capped loader-ring spins since the last
-// read (a ring handshake that never completed; its outputs are wrong);
-// `clear` resets it. Synchronises the device. Returns hipError_t as int.
+// clearing read (a handshake that took the direct-load fallback; outputs
+// right); `clear` resets it. Synchronises the device. Returns hipError_t.
 int read_ring_faults(unsigned* count, int clear);
+// the current device's count of capped hang waits (no fallback: that
+// launch's outputs are wrong), read in order on `stream` after the work
+// already there, which this waits for (nullptr: on the library's own
+// non-blocking stream, ordered after nothing); `clear` resets it. Returns
+// hipError_t as int.
+int read_hang_faults(void* stream, unsigned* count, int clear);
 // occupancy of the GF kernel for a given input count (blocks per CU)
 int gf_blocks_per_cu(int nin);
 // 1 in the test twin library (built with REDSET_HIP_TEST_KNOBS), else 0

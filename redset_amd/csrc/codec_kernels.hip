@@ -39,12 +39,14 @@ int jobs_per_launch(const Launch& L) {
   return L.sequential == kJobsInLaunches ? std::max(1, L.group) : L.njobs;
 }
 
-// Capped loader-ring spins (codec_device.h ring_sweep), one word per device:
-// the kernels get its address in GfLaunch / XorLaunch::fault. Launches come
-// from several threads (the pipeline's compute thread, per-rank backends,
-// callers), so the per-device address cache is atomic; a racing first
-// lookup resolves the same address twice, which is harmless.
-__device__ unsigned g_ring_fault;
+// The kernels' fault words, two per device: [0] capped loader-ring spins
+// (codec_device.h ring_sweep; a fallback ran, outputs right), [1] capped hang
+// waits (no fallback, outputs wrong; kRingHangCap). The kernels get the
+// address in GfLaunch / XorLaunch::fault. Launches come from several threads
+// (the pipeline's compute thread, per-rank backends, callers), so the
+// per-device address cache is atomic; a racing first lookup resolves the
+// same address twice, which is harmless.
+__device__ unsigned g_ring_fault[2];
 
 unsigned* ring_fault_word() {
   static std::atomic<unsigned*> addr[64];
@@ -64,31 +66,35 @@ unsigned* ring_fault_word() {
 // the loader ring's poll cap and a claimer delay from the environment
 // (REDSET_HIP_TEST_SPIN_CAP, REDSET_HIP_TEST_CLAIM_DELAY), so the suite can
 // drive the ring's fallbacks and the claimed kernel's claim/record window on
-// every launch. The product library reads no environment here.
-unsigned spin_cap() {
+// every launch. Read at every launch, so one test process can change them.
+// The product library reads no environment here.
+unsigned test_env(const char* name, unsigned dflt) {
 #if REDSET_HIP_TEST_KNOBS
-  static const unsigned cap = [] {
-    const char* s = std::getenv("REDSET_HIP_TEST_SPIN_CAP");
-    const long v = s ? std::atol(s) : 0;
-    return v > 0 ? static_cast<unsigned>(v) : 1u << 24;
-  }();
-  return cap;
+  const char* s = std::getenv(name);
+  const long v = s ? std::atol(s) : 0;
+  return v > 0 ? static_cast<unsigned>(v) : dflt;
 #else
-  return 1u << 24;
+  (void) name;
+  return dflt;
 #endif
 }
 
-unsigned claim_delay() {
-#if REDSET_HIP_TEST_KNOBS
-  static const unsigned d = [] {
-    const char* s = std::getenv("REDSET_HIP_TEST_CLAIM_DELAY");
-    const long v = s ? std::atol(s) : 0;
-    return v > 0 ? static_cast<unsigned>(v) : 0u;
-  }();
-  return d;
-#else
-  return 0;
-#endif
+unsigned spin_cap() { return test_env("REDSET_HIP_TEST_SPIN_CAP", 1u << 24); }
+unsigned claim_delay() { return test_env("REDSET_HIP_TEST_CLAIM_DELAY", 0); }
+
+// Test builds: the hang cap (REDSET_HIP_TEST_HANG_CAP polls) and the
+// loader's table delay (REDSET_HIP_TEST_TABLE_DELAY), so the suite can make
+// the hang waits fire (codec_device.h kRingHangCap).
+unsigned hang_cap() { return test_env("REDSET_HIP_TEST_HANG_CAP", 1u << 26); }
+unsigned table_delay() { return test_env("REDSET_HIP_TEST_TABLE_DELAY", 0); }
+
+template <class Launch>
+void set_launch_knobs(Launch& one) {
+  one.fault = ring_fault_word();
+  one.spin_cap = spin_cap();
+  one.claim_delay = claim_delay();
+  one.hang_cap = hang_cap();
+  one.table_delay = table_delay();
 }
 }  // namespace
 
@@ -100,6 +106,38 @@ int read_ring_faults(unsigned* count, int clear) {
   if (e == hipSuccess && clear && v) {
     const unsigned zero = 0;
     e = hipMemcpyToSymbol(HIP_SYMBOL(g_ring_fault), &zero, sizeof(zero), 0, hipMemcpyHostToDevice);
+  }
+  if (count) *count = v;
+  return e;
+}
+
+// a non-blocking stream of the library's own per device, for reads of the
+// hang word that must not wait for unrelated work (created once, kept)
+static hipStream_t own_stream() {
+  static std::atomic<hipStream_t> streams[64];
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
+  hipStream_t s = streams[dev].load(std::memory_order_acquire);
+  if (!s) {
+    hipStream_t made = nullptr;
+    if (hipStreamCreateWithFlags(&made, hipStreamNonBlocking) != hipSuccess) return nullptr;
+    if (streams[dev].compare_exchange_strong(s, made, std::memory_order_acq_rel)) s = made;
+    else (void) hipStreamDestroy(made);  // another thread made one first
+  }
+  return s;
+}
+
+int read_hang_faults(void* stream, unsigned* count, int clear) {
+  const hipStream_t s = stream ? static_cast<hipStream_t>(stream) : own_stream();
+  if (!s) return hipErrorInvalidResourceHandle;
+  unsigned v = 0;
+  const size_t off = sizeof(unsigned);
+  hipError_t e = hipMemcpyFromSymbolAsync(&v, HIP_SYMBOL(g_ring_fault), sizeof(v), off, hipMemcpyDeviceToHost, s);
+  if (e == hipSuccess) e = hipStreamSynchronize(s);
+  if (e == hipSuccess && clear && v) {
+    const unsigned zero = 0;
+    e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_ring_fault), &zero, sizeof(zero), off, hipMemcpyHostToDevice, s);
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
   }
   if (count) *count = v;
   return e;
@@ -143,9 +181,7 @@ int launch_gf(const GfLaunch& L, void* stream) {
   for (int j = 0; j < L.njobs; j += per) {
     GfLaunch one = L;
     one.job0 = j;
-    one.fault = ring_fault_word();
-    one.spin_cap = spin_cap();
-    one.claim_delay = claim_delay();
+    set_launch_knobs(one);
     if (L.sequential == kJobsStreamed || L.sequential == kJobsClaimed) one.njobs = std::min(per, L.njobs - j);
     if (L.sequential == kJobsClaimed && L.claim) {
       // the claim queues start at zero for every launch, whatever an earlier
@@ -168,8 +204,7 @@ int launch_gf_single(const GfLaunch& L, const GfJob& J, void* stream) {
   if (L.nin < 1 || L.nin > kMaxIn || L.nout < 1 || L.nout > kMaxOut) return hipErrorInvalidValue;
   if (L.nbytes == 0) return hipSuccess;
   GfLaunch one = L;
-  one.fault = ring_fault_word();
-  one.spin_cap = spin_cap();
+  set_launch_knobs(one);
   hipLaunchKernelGGL(kernel_set(L.nin).gf_arg[L.nout - 1][L.accumulate ? 1 : 0], dim3(static_cast<unsigned>(L.blocks_per_job)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), one, J);
   return hipGetLastError();
@@ -179,8 +214,7 @@ int launch_xor_single(const XorLaunch& L, const XorJob& J, void* stream) {
   if (L.nin < 1 || L.nin > kMaxIn) return hipErrorInvalidValue;
   if (L.nbytes == 0) return hipSuccess;
   XorLaunch one = L;
-  one.fault = ring_fault_word();
-  one.spin_cap = spin_cap();
+  set_launch_knobs(one);
   hipLaunchKernelGGL(kernel_set(L.nin).xr_arg[L.accumulate ? 1 : 0], dim3(static_cast<unsigned>(L.blocks_per_job)), dim3(kBlock), 0,
                      static_cast<hipStream_t>(stream), one, J);
   return hipGetLastError();
@@ -194,9 +228,7 @@ int launch_xor(const XorLaunch& L, void* stream) {
   for (int j = 0; j < L.njobs; j += per) {
     XorLaunch one = L;
     one.job0 = j;
-    one.fault = ring_fault_word();
-    one.spin_cap = spin_cap();
-    one.claim_delay = claim_delay();
+    set_launch_knobs(one);
     if (L.sequential == kJobsClaimed && L.claim) {
       const hipError_t e = hipMemsetAsync(L.claim, 0, kClaimWords * sizeof(unsigned), static_cast<hipStream_t>(stream));
       if (e != hipSuccess) return e;

@@ -104,11 +104,27 @@ int redset_hip_rank_last_stats(redset_hip_rank_stats* out) {
   return REDSET_SUCCESS;
 }
 
+/* The kernels' hang word (include/redset_hip.h redset_hip_hang_faults) at the
+ * start of the calling thread's backend call: a call during which it moved
+ * fails, because a kernel wait with no fallback gave up and some launch's
+ * outputs are wrong. The failure is this member's alone, after every
+ * collective of the call has run; the caller's AND-reduce of the backends'
+ * results fails redset_apply / redset_recover as a whole
+ * (src/redset_reedsolomon.c:336-341, :1132). */
+static __thread unsigned g_hang0;
+static __thread int g_hang_read;
+
 static double stats_begin(void) {
   memset(&g_stats, 0, sizeof(g_stats));
+  g_hang_read = redset_hip_hang_faults(NULL, &g_hang0, 0) == REDSET_SUCCESS;
   return now_s();
 }
 static int stats_end(double t0, int rc) {
+  unsigned h = 0;
+  if (!rc && (!g_hang_read || redset_hip_hang_faults(NULL, &h, 0) != REDSET_SUCCESS))
+    rc = fail("cannot read the kernels' hang count");
+  else if (!rc && h != g_hang0)
+    rc = fail("a kernel wait hit its hang cap during this call (%u): outputs not trusted", h - g_hang0);
   g_stats.seconds = now_s() - t0;
   return rc;
 }
@@ -412,19 +428,25 @@ static int rs_encode_impl(const redset_hip_rs* rs, MPI_Comm comm, const redset_h
   const int d = p - e;
   const size_t buf = buf_size ? buf_size : DEFAULT_BUF;
   if (buf > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", buf); /* same on every rank */
-  /* the cells of the budget: the two parity buffers (the ring windows are
-   * bounded by MAX_STAGE below) */
-  const size_t B = slice_bytes(buf, chunk_size, (size_t) 2 * e);
+  /* the call's page-locked buffers, in slices of B: the window's own
+   * segments (G), two receive windows (2*G*e) and two parity buffers (2*e).
+   * The slice is cut so that even one-step windows (G = 1) fit SLICE_BUDGET:
+   * (4e + 1) slices */
+  const size_t B = slice_bytes(buf, chunk_size, (size_t) 4 * e + 1);
   /* ring steps staged per window: the d*e slices of a slice's whole ring
    * would need d*e*B of pinned and device memory (O(p*e)); windows of G steps
-   * bound each staging buffer to MAX_STAGE, the reference's own scratch being
-   * e+e+1 slices */
+   * bound each receive window to MAX_STAGE, and all of the call's slice
+   * buffers together to SLICE_BUDGET -- (2e + 1)*G + 2e slices (the
+   * reference's own scratch is e+e+1 slices). RS(8+3) at the default 4 MiB
+   * slice: G = 8 = d, 248 MiB pinned (and as much device memory) */
   size_t stage = MAX_STAGE;
 #if REDSET_HIP_TEST_KNOBS
   /* test builds: the staging bound, for A/B runs (tools/rank_bench.py) */
   if (getenv("REDSET_HIP_TEST_RANK_STAGE_MIB")) stage = (size_t) atoll(getenv("REDSET_HIP_TEST_RANK_STAGE_MIB")) << 20;
 #endif
   int G = (int) (stage / ((size_t) e * B));
+  const size_t fit = SLICE_BUDGET > (size_t) 2 * e * B ? (SLICE_BUDGET - (size_t) 2 * e * B) / ((size_t) (2 * e + 1) * B) : 1;
+  if ((size_t) G > fit) G = (int) fit;
   if (G < 1) G = 1;
   if (G > d) G = d;
 
@@ -1181,17 +1203,22 @@ static int rccl_create(MPI_Comm comm, int p, int r, comm_exchange* X) {
   return 0;
 }
 
-/* The exchange of this decode (collective): the process's mode -- every
- * member must set the same one -- and, for AUTO, RCCL when the members each
- * own a GPU of one node, else the host path. *tr is set for the sharded
+/* The exchange of this call (collective): the process's mode -- every
+ * member must set the same one -- and, for AUTO, RCCL when the call is a
+ * decode (`auto_rccl`) and the members each own a GPU of one node, else the
+ * host path. AUTO keeps the encodes on the host path: north_star asks for
+ * RCCL "only for the multi-rank rebuild case", and an encode over RCCL has
+ * not yet run on a node with a GPU per member; forcing
+ * _SHARDED_RCCL still sends an encode there. *tr is set for the sharded
  * modes; *mpi_t is a transport to destroy after the call (SHARDED_MPI). */
-static int choose_exchange(MPI_Comm comm, int p, int r, int* mode, redset_hip_transport* tr,
+static int choose_exchange(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, redset_hip_transport* tr,
                            redset_hip_mpi_transport** mpi_t) {
   int m[2] = {g_exchange_mode, -g_exchange_mode}, mm[2];
   *mpi_t = NULL;
   if (MPI_Allreduce(m, mm, 2, MPI_INT, MPI_MAX, comm) != MPI_SUCCESS) return fail("MPI_Allreduce failed");
   if (mm[0] != -mm[1]) return fail("members disagree on the rebuild exchange (redset_hip_rank_set_exchange)");
   *mode = m[0];
+  if (*mode == REDSET_HIP_EXCHANGE_AUTO && !auto_rccl) *mode = REDSET_HIP_EXCHANGE_HOST_MPI;
   if (*mode == REDSET_HIP_EXCHANGE_HOST_MPI) return 0;
   if (*mode == REDSET_HIP_EXCHANGE_SHARDED_MPI) {
     /* the sharded plan over MPI with device buffers staged through pinned
@@ -1242,7 +1269,7 @@ static int member_cell(int p, int e, int xor_scheme, int r, int c) {
 static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int p, int r, int e, int missing,
                         const int* lost, int need_rebuild, const redset_hip_io* lofi, const char* chunk_file,
                         int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B,
-                        const redset_hip_transport* tr) {
+                        const redset_hip_transport* tr, redset_hip_mpi_transport* mt) {
   const int d = p - e, ncell = p, world = p;
   const int xor_scheme = rs == NULL;
   size_t win = SHARDED_WINDOW / (size_t) ncell;
@@ -1288,6 +1315,39 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
     if (used) want[member_cell(p, e, xor_scheme, r, c)] = 1;
   }
   for (int m = 0; m < p && host; ++m) host[m] = m;
+  /* the plans of every window before the agreement (planning is local: no
+   * communication, every member the same): buffers b = n & 1 of window n,
+   * for a whole window or the tail one. Over the MPI transport, its staging
+   * and requests are sized here for the largest exchange, so no exchange
+   * allocates (a failed allocation there would leave the peers waiting) */
+  const double tp = now_s();
+  size_t xbytes = 0, xmsgs = 0;
+  for (size_t n = 0; n < nwin && !rc; ++n) {
+    const size_t len = n + 1 == nwin ? tail : win;
+    const int b = (int) (n & 1);
+    redset_hip_sharded** P = &plan[b][len != win];
+    if (*P) continue;
+    redset_hip_shard_layout L = {1, host, slot, 1, len, W, hd[b], hp[b], gd[b], gp[b]};
+    if (encode)
+      rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, tr, NULL, P)
+                      : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, tr, NULL, P);
+    else
+      rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, tr, NULL, P)
+                      : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, tr, NULL, P);
+    redset_hip_sharded_info info;
+    if (!rc && !(rc = redset_hip_sharded_get_info(*P, &info))) {
+      const size_t gb = info.gather_bytes_sent + info.gather_bytes_recv;
+      const size_t rb = info.return_bytes_sent + info.return_bytes_recv;
+      const size_t gm = (size_t) info.gather_messages + (size_t) info.gather_recv_messages;
+      const size_t rm = (size_t) info.return_messages + (size_t) info.return_recv_messages;
+      xbytes = gb > xbytes ? gb : xbytes;
+      xbytes = rb > xbytes ? rb : xbytes;
+      xmsgs = gm > xmsgs ? gm : xmsgs;
+      xmsgs = rm > xmsgs ? rm : xmsgs;
+    }
+  }
+  if (!rc && mt) rc = redset_hip_mpi_transport_reserve(mt, xbytes, xmsgs);
+  g_stats.plan_seconds += now_s() - tp;
   if ((rc = agree_setup(comm, rc))) goto out;
 
   int stopped = 0;
@@ -1297,18 +1357,8 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
     if (n < nwin) {
       /* buffers b were last used by window n - 2, written at window n - 1 */
       if (n >= 2 && !rc && ev_wait(ev[b])) rc = REDSET_FAILURE;
-      /* the plan of buffers b for a whole window, or for the tail window
-       * (planning is local: no communication, every member the same) */
+      /* the plan of buffers b for a whole window, or for the tail window */
       redset_hip_sharded** P = &plan[b][len != win];
-      if (!rc && !*P) {
-        redset_hip_shard_layout L = {1, host, slot, 1, len, W, hd[b], hp[b], gd[b], gp[b]};
-        if (encode)
-          rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, tr, NULL, P)
-                          : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, tr, NULL, P);
-        else
-          rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, tr, NULL, P)
-                          : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, tr, NULL, P);
-      }
       uint8_t* img = h_img[b];
       for (int x = 0; x < ncell && !rc; ++x) {
         if (!want[x]) continue;
@@ -1331,6 +1381,7 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
       }
       hipStream_t s = S.stream;
       if (!rc) rc = injected_device_failure(comm);
+      double tc = now_s();
       for (int x = 0; x < ncell && !rc; ++x) {
         if (!want[x]) continue;
         uint8_t* dst = x < d ? hd[b] + (size_t) x * W : hp[b] + (size_t) (x - d) * W;
@@ -1340,15 +1391,23 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
           rc = fail("H2D copy failed");
         g_stats.h2d_bytes += WW;
       }
+      g_stats.copy_seconds += now_s() - tc;
       /* the exchange runs whatever this member's state since the agreement:
        * its peers are in it (a member whose copies failed sends what its
        * buffers hold, and every member stops at the next window's agreement) */
-      if (redset_hip_sharded_execute(*P, s) != 0 && !rc) rc = REDSET_FAILURE;
+      const double tx = now_s();
+      if (!*P) {
+        if (!rc) rc = fail("sharded window without a plan");
+      } else if (redset_hip_sharded_execute(*P, s) != 0 && !rc) {
+        rc = REDSET_FAILURE;
+      }
+      g_stats.exchange_seconds += now_s() - tx;
       redset_hip_sharded_info info;
       if (!rc && redset_hip_sharded_get_info(*P, &info) == 0) {
         g_stats.sent_bytes += info.gather_bytes_sent + info.return_bytes_sent;
         g_stats.recv_bytes += info.gather_bytes_recv + info.return_bytes_recv;
       }
+      tc = now_s();
       for (int x = encode ? d : 0; x < ncell && !rc && (need_rebuild || encode); ++x) {
         const uint8_t* src = x < d ? hd[b] + (size_t) x * W : hp[b] + (size_t) (x - d) * W;
         const size_t spitch = (size_t) (x < d ? d : e) * W;
@@ -1357,6 +1416,7 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
           rc = fail("D2H copy failed");
         g_stats.d2h_bytes += WW;
       }
+      g_stats.copy_seconds += now_s() - tc;
       if (!rc && hipEventRecord(ev[b], s) != hipSuccess) rc = fail("hipEventRecord failed");
     }
     /* window n - 1's rebuilt cells (encode: parity cells), after the header
@@ -1411,7 +1471,7 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   int mode;
   redset_hip_transport tr;
   redset_hip_mpi_transport* mt = NULL;
-  if (choose_exchange(comm, p, r, &mode, &tr, &mt)) {
+  if (choose_exchange(comm, p, r, 1, &mode, &tr, &mt)) {
     redset_hip_mpi_transport_destroy(mt);
     return REDSET_FAILURE;
   }
@@ -1420,7 +1480,7 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
                ? rs_decode_host(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
                                 header, hrc, chunk_size, slice_bytes(B, chunk_size, (size_t) (4 * p + 2 * missing)))
                : sharded_slot(0, rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
-                              header, hrc, chunk_size, B, &tr);
+                              header, hrc, chunk_size, B, &tr, mt);
   redset_hip_mpi_transport_destroy(mt);
   return stats_end(t0, rc);
 }
@@ -1442,7 +1502,7 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   int mode;
   redset_hip_transport tr;
   redset_hip_mpi_transport* mt = NULL;
-  if (choose_exchange(comm, p, r, &mode, &tr, &mt)) {
+  if (choose_exchange(comm, p, r, 1, &mode, &tr, &mt)) {
     redset_hip_mpi_transport_destroy(mt);
     return REDSET_FAILURE;
   }
@@ -1450,16 +1510,16 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
                ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B)
                : sharded_slot(0, NULL, comm, p, r, 1, 1, &root, r == root, lofi, chunk_file, fd_chunk, header, hrc,
-                              chunk_size, B, &tr);
+                              chunk_size, B, &tr, mt);
   redset_hip_mpi_transport_destroy(mt);
   return stats_end(t0, rc);
 }
 
-/* The encodes pick their exchange as the decodes do (choose_exchange): on a
- * node whose members each own a GPU the encode runs as the sharded plan over
- * RCCL -- every data cell's column slices gathered onto the GPUs, gf_mac (or
- * the XOR) there, the parity slices returned to their holders -- instead of
- * the host ring (src/redset_reedsolomon.c:329-377, src/redset_xor.c:251-285). */
+/* The encodes take the host ring under AUTO (choose_exchange) and the
+ * sharded plan when a sharded mode is set: every data cell's column slices
+ * gathered onto the GPUs, gf_mac (or the XOR) there, the parity slices
+ * returned to their holders, instead of the host ring
+ * (src/redset_reedsolomon.c:329-377, src/redset_xor.c:251-285). */
 static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file,
                        int fd_chunk, size_t chunk_size, size_t buf_size) {
   int p, r, e = 1;
@@ -1477,7 +1537,7 @@ static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_
   int mode;
   redset_hip_transport tr;
   redset_hip_mpi_transport* mt = NULL;
-  if (choose_exchange(comm, p, r, &mode, &tr, &mt)) {
+  if (choose_exchange(comm, p, r, 0, &mode, &tr, &mt)) {
     redset_hip_mpi_transport_destroy(mt);
     return REDSET_FAILURE;
   }
@@ -1490,7 +1550,8 @@ static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_
     /* a bad fd on one member is agreed on inside, not returned early */
     off_t header;
     const int hrc = header_size(fd_chunk, chunk_file, &header);
-    rc = sharded_slot(1, rs, comm, p, r, e, 0, NULL, 0, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B, &tr);
+    rc = sharded_slot(1, rs, comm, p, r, e, 0, NULL, 0, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B, &tr,
+                      mt);
   }
   redset_hip_mpi_transport_destroy(mt);
   return rc;
@@ -1524,20 +1585,8 @@ struct redset_hip_mpi_transport {
   int req_cap;
 };
 
-/* Every message of the exchange is posted and waited for even after a HIP
- * error on this member (its peers are in the same exchange and would hang,
- * src/redset_reedsolomon.c:338-342): the error is returned at the end, and
- * the bytes this member sent are unspecified. */
-static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream) {
-  struct redset_hip_mpi_transport* T = (struct redset_hip_mpi_transport*) ctx;
-  hipStream_t s = (hipStream_t) stream;
-  int rc = 0;
-  size_t need = 0, nreq = 0;
-  for (int i = 0; i < n; ++i)
-    if (x[i].peer != T->rank) {
-      need += x[i].len;
-      nreq += (x[i].len + MPI_PIECE - 1) / MPI_PIECE;
-    }
+/* staging and requests for `need` bytes and `nreq` MPI requests */
+static int mpi_transport_size(struct redset_hip_mpi_transport* T, size_t need, size_t nreq) {
   if (T->device && need > T->stage_len) {
     if (T->stage) T->stage_pinned ? (void) hipHostFree(T->stage) : free(T->stage);
     T->stage = NULL;
@@ -1548,19 +1597,51 @@ static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream
     if (!T->stage) return fail("mpi transport: out of host memory (%zu)", need);
     T->stage_len = need;
   }
+  if (nreq > (size_t) T->req_cap) {
+    MPI_Request* r = realloc(T->req, sizeof(*r) * nreq);
+    if (!r) return fail("mpi transport: out of host memory (%zu requests)", nreq);
+    T->req = r;
+    T->req_cap = (int) nreq;
+  }
+  return 0;
+}
+
+int redset_hip_mpi_transport_reserve(redset_hip_mpi_transport* T, size_t bytes, size_t messages) {
+  if (!T) return fail("mpi_transport_reserve: null transport");
+  /* messages above MPI_PIECE go in pieces: at most bytes / MPI_PIECE more */
+  return mpi_transport_size(T, bytes, messages + bytes / MPI_PIECE + 1) ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+/* Every message of the exchange is posted and waited for even after a HIP
+ * error on this member (its peers are in the same exchange and would hang,
+ * src/redset_reedsolomon.c:338-342): the error is returned at the end, and
+ * the bytes this member sent are unspecified. Only buffers that were not
+ * reserved (redset_hip_mpi_transport_reserve) and then fail to allocate
+ * return before the messages are posted. Where the host thread waits goes to
+ * the call's stats (redset_hip_rank_last_stats): the GPU work that feeds
+ * the exchange (gpu_seconds), the staging copies (stage_seconds), MPI
+ * (mpi_seconds). */
+static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream) {
+  struct redset_hip_mpi_transport* T = (struct redset_hip_mpi_transport*) ctx;
+  hipStream_t s = (hipStream_t) stream;
+  int rc = 0;
+  size_t need = 0, nreq = 0;
+  for (int i = 0; i < n; ++i)
+    if (x[i].peer != T->rank) {
+      need += x[i].len;
+      nreq += (x[i].len + MPI_PIECE - 1) / MPI_PIECE;
+    }
+  if (mpi_transport_size(T, need, nreq)) return REDSET_FAILURE;
   /* work already on the stream produced the send buffers -- in host mode
    * too, where a HIP compute over page-locked slabs may still be writing
    * them, on the null stream as well (device_buffers = 2); a host-only
    * caller (device_buffers = 0, no stream) needs no HIP runtime */
+  double t0 = now_s();
   if ((T->device || T->hip_host || s) && hipStreamSynchronize(s) != hipSuccess)
     rc = fail("mpi transport: stream sync failed");
-  if ((int) nreq > T->req_cap) {
-    MPI_Request* r = realloc(T->req, sizeof(*r) * nreq);
-    if (!r) return fail("out of host memory");
-    T->req = r;
-    T->req_cap = (int) nreq;
-  }
+  g_stats.gpu_seconds += now_s() - t0;
   /* local copies, and (device mode) every send staged to host */
+  t0 = now_s();
   size_t off = 0;
   for (int i = 0; i < n; ++i) {
     if (x[i].peer == T->rank) {
@@ -1581,6 +1662,7 @@ static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream
     off += x[i].len;
   }
   if (!rc && T->device && hipStreamSynchronize(s) != hipSuccess) rc = fail("mpi transport: stream sync failed");
+  g_stats.stage_seconds += now_s() - t0;
   int k = 0;
   off = 0;
   for (int i = 0; i < n; ++i) {
@@ -1596,20 +1678,26 @@ static int mpi_exchange(void* ctx, const redset_hip_xfer* x, int n, void* stream
     }
     off += x[i].len;
   }
-  if (MPI_Waitall(k, T->req, MPI_STATUSES_IGNORE) != MPI_SUCCESS) return fail("mpi transport: MPI_Waitall failed");
+  t0 = now_s();
+  const int mrc = MPI_Waitall(k, T->req, MPI_STATUSES_IGNORE);
+  g_stats.mpi_seconds += now_s() - t0;
+  if (mrc != MPI_SUCCESS) return fail("mpi transport: MPI_Waitall failed");
   if (!T->device || rc) return rc;
+  t0 = now_s();
   off = 0;
-  for (int i = 0; i < n; ++i) {
+  for (int i = 0; i < n && !rc; ++i) {
     if (x[i].peer == T->rank) {
       ++i;
       continue;
     }
     if (!x[i].send && hipMemcpyAsync(x[i].buf, T->stage + off, x[i].len, hipMemcpyHostToDevice, s) != hipSuccess)
-      return fail("mpi transport: H2D failed");
+      rc = fail("mpi transport: H2D failed");
     off += x[i].len;
   }
   /* the staging buffer is reused by the next exchange */
-  return hipStreamSynchronize(s) == hipSuccess ? 0 : fail("mpi transport: stream sync failed");
+  if (!rc && hipStreamSynchronize(s) != hipSuccess) rc = fail("mpi transport: stream sync failed");
+  g_stats.stage_seconds += now_s() - t0;
+  return rc;
 }
 
 int redset_hip_mpi_transport_create(MPI_Comm comm, int device_buffers, redset_hip_transport* out,

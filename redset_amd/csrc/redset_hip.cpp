@@ -106,8 +106,9 @@ constexpr size_t kSequentialMinCell = 24u << 20;
 
 // can_stream: the kernel has a streamed path for these jobs (GF: <= 8
 // inputs, XOR: <= 8 inputs, both over whole 16-B vectors); can_claim: a
-// claimed one (GF only); claim_default / stream_default: which is the
-// default for big cells.
+// claimed one (the same jobs: GF and XOR of <= 8 inputs over whole 16-B
+// vectors; XOR claiming is off by default, xor_claim_default);
+// claim_default / stream_default: which is the default for big cells.
 int sequential_jobs(int njobs, size_t nbytes, bool can_stream, bool can_claim, bool claim_default,
                      bool stream_default) {
   if (njobs < 2) return 0;
@@ -428,6 +429,10 @@ int redset_hip_test_build(void) { return redset_hip::test_knobs(); }
 int redset_hip_ring_faults(unsigned* count, int clear) {
   if (!count) return fail("ring_faults: null argument");
   return hip_check(static_cast<hipError_t>(redset_hip::read_ring_faults(count, clear)), "ring_faults");
+}
+int redset_hip_hang_faults(void* stream, unsigned* count, int clear) {
+  if (!count) return fail("hang_faults: null argument");
+  return hip_check(static_cast<hipError_t>(redset_hip::read_hang_faults(stream, count, clear)), "hang_faults");
 }
 const char* redset_hip_last_error(void) { return redset_hip::last_error(); }
 int redset_hip_record_error(const char* msg) { return fail("%s", msg ? msg : "unknown error"); }

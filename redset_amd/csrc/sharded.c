@@ -122,7 +122,7 @@ static int ex_copy(exch* X, unsigned char* dst, const unsigned char* src, size_t
 
 /* message statistics of one phase (the info block) */
 typedef struct {
-  int* messages;
+  int *messages, *recv_messages;
   unsigned long long *sent, *recvd, *local, *max_msg, *min_msg;
 } xstats;
 
@@ -145,6 +145,7 @@ static int ex_flatten(exch* X, xlist* out, const xstats* st) {
     for (int i = 0; i < X->recv[g].n; ++i) {
       if (xl_push(out, X->recv[g].v[i])) return REDSET_FAILURE;
       *st->recvd += X->recv[g].v[i].len;
+      ++*st->recv_messages;
     }
   }
   return 0;
@@ -394,10 +395,12 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
   /* set by set, so a set's exchanges can run on their own (pipelined execute) */
   for (int k = 0; k < L->nsets && !rc; ++k) {
     rc = plan_gather(&C, k, &G);
-    const xstats gs = {&P->info.gather_messages, &P->info.gather_bytes_sent, &P->info.gather_bytes_recv,
-                       &P->info.local_bytes, &P->info.gather_msg_max, &P->info.gather_msg_min};
-    const xstats rs_ = {&P->info.return_messages, &P->info.return_bytes_sent, &P->info.return_bytes_recv,
-                        &P->info.local_bytes, &P->info.return_msg_max, &P->info.return_msg_min};
+    const xstats gs = {&P->info.gather_messages, &P->info.gather_recv_messages, &P->info.gather_bytes_sent,
+                       &P->info.gather_bytes_recv, &P->info.local_bytes, &P->info.gather_msg_max,
+                       &P->info.gather_msg_min};
+    const xstats rs_ = {&P->info.return_messages, &P->info.return_recv_messages, &P->info.return_bytes_sent,
+                        &P->info.return_bytes_recv, &P->info.local_bytes, &P->info.return_msg_max,
+                        &P->info.return_msg_min};
     if (!rc) rc = ex_flatten(&G, &P->gather, &gs);
     if (!rc) rc = plan_return(&C, k, &R);
     if (!rc) rc = ex_flatten(&R, &P->ret, &rs_);

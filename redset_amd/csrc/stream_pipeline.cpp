@@ -32,6 +32,7 @@
 #include <thread>
 #include <vector>
 
+#include "codec_kernels.h"
 #include "redset_hip.h"
 #include "stripe_map.h"
 
@@ -244,6 +245,19 @@ constexpr int kSlots = 4;
 
 int hip_ok(hipError_t e, const char* what) { return e == hipSuccess ? 0 : fail("%s: %s", what, hipGetErrorString(e)); }
 
+// The kernels' hang word (include/redset_hip.h redset_hip_hang_faults), read
+// in order on `s`: at the start of a call, and after its last sync, where a
+// count that moved fails the call -- a wait with no fallback gave up, so
+// some launch's outputs are wrong and the call must not report success.
+int hang_mark(hipStream_t s, unsigned* v) {
+  return hip_ok(static_cast<hipError_t>(redset_hip::read_hang_faults(s, v, 0)), "hang-fault read");
+}
+int hang_check(hipStream_t s, unsigned before) {
+  unsigned now = before;
+  if (int rc = hang_mark(s, &now)) return rc;
+  return now == before ? 0 : fail("a kernel wait hit its hang cap (%u since the call began): outputs not trusted", now - before);
+}
+
 // Zero copy: when every cell of every stripe is page-locked host memory
 // (io->map gives its address, contiguous over the whole cell), the gf_mac /
 // xor kernel reads its inputs and writes its outputs over PCIe directly --
@@ -291,6 +305,8 @@ int try_zero_copy(const std::vector<StripeMap>& maps, size_t chunk, const redset
   hipStream_t s = cache.take_stream();
   hipEvent_t e0 = nullptr, e1 = nullptr;
   int rc = s ? 0 : fail("hipStreamCreate failed");
+  unsigned hang0 = 0;
+  rc = rc ? rc : hang_mark(s, &hang0);
   rc = rc ? rc : hip_ok(hipEventCreate(&e0), "event");
   rc = rc ? rc : hip_ok(hipEventCreate(&e1), "event");
   rc = rc ? rc : hip_ok(hipEventRecord(e0, s), "event record");
@@ -303,6 +319,7 @@ int try_zero_copy(const std::vector<StripeMap>& maps, size_t chunk, const redset
   }
   rc = rc ? rc : hip_ok(hipEventRecord(e1, s), "event record");
   rc = rc ? rc : hip_ok(hipStreamSynchronize(s), "stream synchronize");
+  rc = rc ? rc : hang_check(s, hang0);
   float ms = 0;
   if (rc == 0 && hipEventElapsedTime(&ms, e0, e1) == hipSuccess) st->gpu_seconds = ms * 1e-3;
   const bool synced = s && hipStreamSynchronize(s) == hipSuccess;
@@ -353,6 +370,8 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
   ResourceCache& cache = ResourceCache::get();
   hipStream_t s_in = cache.take_stream(), s_comp = cache.take_stream(), s_out = cache.take_stream();
   int rc = (s_in && s_comp && s_out) ? 0 : fail("hipStreamCreate failed");
+  unsigned hang0 = 0;
+  rc = rc ? rc : hang_mark(s_comp, &hang0);
   auto buf = [&](uint8_t** p, size_t* have, size_t n, bool dev) {
     if (rc) return;
     *p = static_cast<uint8_t*>(cache.take_buf(n, dev, have));
@@ -508,6 +527,7 @@ int run_pipeline(const std::vector<StripeMap>& maps, size_t chunk, size_t slice,
   bool ok = rc == 0 && io_err.load() != 2;
   for (hipStream_t s : {s_in, s_comp, s_out})
     if (s && hipStreamSynchronize(s) != hipSuccess) ok = false;
+  if (ok) rc = hang_check(s_comp, hang0);
   for (Slot& S : slots) {
     cache.give_buf(S.h_in, S.n_h_in, false, ok);
     cache.give_buf(S.h_out, S.n_h_out, false, ok);

@@ -86,6 +86,11 @@ def _no_ring_faults(request):
     import redset_amd
 
     n = redset_amd.ring_faults()
+    # waits with no fallback (include/redset_hip.h redset_hip_hang_faults)
+    # never give up in a healthy run, the 4-poll fallback run included (its
+    # hang cap stays at 2^26); tests that make them fire clear the count
+    hangs = redset_amd.hang_faults()
+    assert hangs == 0, f"{hangs} kernel waits hit their hang cap (outputs of those launches are wrong)"
     if FALLBACK_RUN:
         _fallback_faults[0] += n
         return

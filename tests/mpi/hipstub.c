@@ -76,3 +76,17 @@ int redset_hip_xor_combine(const unsigned char* const* in, int nin, unsigned cha
   }
   return 0;
 }
+
+/* the kernels' hang count (include/redset_hip.h redset_hip_hang_faults):
+ * 0, unless HIPSTUB_HANG_RANK names this process's MPI rank (PMI_RANK), whose
+ * count then moves on every read -- a hang-capped kernel wait in every call,
+ * which the backends must turn into REDSET_FAILURE */
+int redset_hip_hang_faults(void* s, unsigned* count, int clear) {
+  static unsigned reads;
+  (void) s;
+  (void) clear;
+  const char* want = getenv("HIPSTUB_HANG_RANK");
+  const char* me = getenv("PMI_RANK");
+  *count = (want && me && atoi(want) == atoi(me)) ? reads++ : 0;
+  return 0;
+}

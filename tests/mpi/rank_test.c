@@ -11,6 +11,7 @@
  * (written by tests/test_gpu_mpi.py). Exit 0 iff every rank succeeded.
  * RANK_TEST_EXCHANGE=host|sharded-mpi|rccl: the rebuild's exchange
  * (redset_hip_rank_set_exchange; default auto). Rank 0 prints the one used.
+ * RANK_TEST_DEVICE_PER_RANK=1: rank r on GPU r mod (GPUs).
  * RANK_TEST_FAIL_READ=<rank>: that rank's logical-file reads fail from the
  * second call on (an I/O error in the middle of the collective loop).
  * The HIP runtime is initialised before the timed call (an application that
@@ -71,20 +72,23 @@ static const char* exchange_name(int m) {
 /* the last call's accounting (redset_hip_rank_last_stats), max and sum over
  * the ranks, as one JSON line from rank 0 (tools/rank_bench.py reads it) */
 static void print_stats(int rank, const char* tag) {
-  static const char* names[] = {"seconds", "read_seconds", "mpi_seconds", "gpu_seconds", "write_seconds",
-                                "read_bytes", "sent_bytes", "recv_bytes", "h2d_bytes", "d2h_bytes", "write_bytes"};
+  enum { NS = 15 };
+  static const char* names[NS] = {"seconds", "read_seconds", "mpi_seconds", "gpu_seconds", "write_seconds",
+                                  "read_bytes", "sent_bytes", "recv_bytes", "h2d_bytes", "d2h_bytes", "write_bytes",
+                                  "stage_seconds", "copy_seconds", "plan_seconds", "exchange_seconds"};
   redset_hip_rank_stats st;
   memset(&st, 0, sizeof(st));
   (void) redset_hip_rank_last_stats(&st);
-  double v[11] = {st.seconds, st.read_seconds, st.mpi_seconds, st.gpu_seconds, st.write_seconds,
+  double v[NS] = {st.seconds, st.read_seconds, st.mpi_seconds, st.gpu_seconds, st.write_seconds,
                   (double) st.read_bytes, (double) st.sent_bytes, (double) st.recv_bytes, (double) st.h2d_bytes,
-                  (double) st.d2h_bytes, (double) st.write_bytes};
-  double mx[11], sm[11];
-  MPI_Reduce(v, mx, 11, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
-  MPI_Reduce(v, sm, 11, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
+                  (double) st.d2h_bytes, (double) st.write_bytes, st.stage_seconds, st.copy_seconds,
+                  st.plan_seconds, st.exchange_seconds};
+  double mx[NS], sm[NS];
+  MPI_Reduce(v, mx, NS, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
+  MPI_Reduce(v, sm, NS, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);
   if (rank != 0) return;
   printf("rank_stats %s {", tag);
-  for (int i = 0; i < 11; ++i) printf("%s\"%s\": [%.15g, %.15g]", i ? ", " : "", names[i], mx[i], sm[i]);
+  for (int i = 0; i < NS; ++i) printf("%s\"%s\": [%.15g, %.15g]", i ? ", " : "", names[i], mx[i], sm[i]);
   printf("}\n");
 }
 
@@ -114,6 +118,13 @@ int main(int argc, char** argv) {
   int rank, ranks;
   MPI_Comm_rank(MPI_COMM_WORLD, &rank);
   MPI_Comm_size(MPI_COMM_WORLD, &ranks);
+  /* RANK_TEST_DEVICE_PER_RANK=1: rank r uses GPU r mod (GPUs), the layout of
+   * a node with a GPU per member (where AUTO's decode takes RCCL) */
+  if (getenv("RANK_TEST_DEVICE_PER_RANK")) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1 || hipSetDevice(rank % ndev) != hipSuccess)
+      MPI_Abort(MPI_COMM_WORLD, 7);
+  }
   if (argc < 6) {
     if (rank == 0) fprintf(stderr, "usage: %s rs|xor encode|rebuild encoding dir buf [lost...]\n", argv[0]);
     MPI_Abort(MPI_COMM_WORLD, 2);

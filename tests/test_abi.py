@@ -60,6 +60,7 @@ def test_mpi_library_exports_every_declared_symbol(hiplib):
     text = re.sub(r"/\*.*?\*/", "", open(mpi_h).read(), flags=re.S)
     declared = sorted(set(re.findall(r"\b(redset_hip_\w+)\s*\(", text)))
     assert declared == ["redset_hip_mpi_transport_create", "redset_hip_mpi_transport_destroy",
+                        "redset_hip_mpi_transport_reserve",
                         "redset_hip_rank_last_exchange", "redset_hip_rank_last_stats",
                         "redset_hip_rank_scratch_release",
                         "redset_hip_rank_set_exchange", "redset_hip_rs_decode_rank", "redset_hip_rs_encode_rank",

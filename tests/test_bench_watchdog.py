@@ -39,3 +39,41 @@ def test_watchdog_after_print_exits_without_second_line():
 def test_other_ranks_print_nothing():
     r = _run("import bench\nbench.sharded_expired({'value': 1.0}, 3, 1.0)\n")
     assert r.returncode == 3 and r.stdout == ""
+
+
+def test_relay_passes_one_result_line():
+    """self_launch's relay: rank 0's result line to stdout once, every other
+    line (logs, a second JSON line) to stderr."""
+    r = _run("import bench, io\n"
+             "out, err = io.StringIO(), io.StringIO()\n"
+             "lines = ['log a\\n', '{\"metric\": \"m\", \"value\": 1}\\n', '{\"metric\": \"m\", \"value\": 2}\\n',"
+             " '{not json\\n']\n"
+             "seen = bench.relay(lines, out, err)\n"
+             "print(seen, repr(out.getvalue()), repr(err.getvalue()))\n")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip() == ("True '{\"metric\": \"m\", \"value\": 1}\\n' "
+                                "'log a\\n{\"metric\": \"m\", \"value\": 2}\\n{not json\\n'")
+
+
+def test_self_launch_relays_child_line_and_status(tmp_path):
+    """The launcher runs its ranks as one child process and returns the
+    child's status; no result line is a failure even with status 0, and a
+    child past the timeout is stopped."""
+    ok = tmp_path / "ok.py"
+    ok.write_text("import json; print('rank log'); print(json.dumps({'metric': 'm', 'value': 5}))\n")
+    silent = tmp_path / "silent.py"
+    silent.write_text("print('nothing to report')\n")
+    hang = tmp_path / "hang.py"
+    hang.write_text("import time; time.sleep(60)\n")
+    code = ("import bench, sys\n"
+            f"rc1 = bench.self_launch([], 2, 30, cmd=[sys.executable, {str(ok)!r}])\n"
+            f"rc2 = bench.self_launch([], 2, 30, cmd=[sys.executable, {str(silent)!r}])\n"
+            f"rc3 = bench.self_launch([], 2, 2, cmd=[sys.executable, {str(hang)!r}])\n"
+            "print('rcs', rc1, rc2, rc3)\n")
+    r = _run(code)
+    assert r.returncode == 0, r.stderr
+    out = r.stdout.strip().splitlines()
+    assert json.loads(out[0]) == {"metric": "m", "value": 5}
+    assert "printed no result line" in out[1] and "printed no result line" in out[2]
+    assert out[3] == "rcs 0 1 -9"
+    assert "rank log" in r.stderr

@@ -1,0 +1,70 @@
+"""bench.py as the driver runs it, on the one-GPU box.
+
+* `--gpus 2` WITHOUT torchrun: bench.py starts its two ranks itself (one
+  torch.distributed.run child, before it touches the GPU), the ranks share the
+  box's GPU over gloo, and exactly one JSON line comes back whose sharded leg
+  (configs[3], the column-sharded rebuild, src/redset_reedsolomon.c:646-733
+  replaced) is bit-exact and carries its message counts and HBM fraction.
+* `--gpus 1`: the sharded leg runs at N=1 over the world-1 RCCL transport
+  (configs[3]'s base point) and is bit-exact.
+Small chunks keep both runs to seconds (gloo moves device tensors at tens of
+MB/s); the CPU baseline, pair sweep and XOR leg are off.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SMALL = ["--steps", "2", "--warmup", "1", "--chunk-mib", "0.5", "--cpu-baseline", "0", "--pairs", "0", "--xor", "0"]
+
+
+def _bench(args, timeout):
+    from conftest import gpu_available
+
+    if not gpu_available():
+        pytest.skip("needs an MI355X")
+    env = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR",
+                                                             "MASTER_PORT")}
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py")] + args, cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=timeout)
+    lines = [ln for ln in r.stdout.splitlines() if ln.strip()]
+    assert r.returncode == 0, (r.stdout[-3000:], r.stderr[-6000:])
+    assert len(lines) == 1, r.stdout[-3000:]
+    return json.loads(lines[0])
+
+
+def _check_sharded(sh, world):
+    assert "error" not in sh, sh
+    assert sh["bit_exact"] is True
+    assert sh["value"] > 0 and 0 < sh["frac_of_hbm"] < 1
+    assert sh["hbm_peak_GBps"] == world * 8000.0
+    msgs = sh["exchange"]["messages_per_gpu"]["rebuild"]
+    if world > 1:
+        # every GPU gathers slices from its peer and returns rebuilt slices
+        assert msgs["gather_messages"] > 0 and msgs["return_messages"] > 0, msgs
+        assert sh["exchange"]["bytes_sent_per_gpu_per_step"] > 0
+    else:
+        assert msgs["gather_messages"] == 0 and msgs["return_messages"] == 0, msgs
+        assert sh["roofline"]["bound"] == "hbm" and sh["roofline"]["local_copy_bytes_per_step"] > 0
+
+
+@pytest.mark.timeout(420)
+def test_bench_two_ranks_self_launched_over_gloo():
+    line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--sharded-timeout", "300"] + SMALL, 400)
+    assert line["n_gpus"] == 2 and line["round_trip_bit_exact"] is True
+    assert line["config"]["sets"] == 2
+    assert line["config"]["scaling_value"].startswith("sharded.value")
+    _check_sharded(line["sharded"], 2)
+
+
+@pytest.mark.timeout(300)
+def test_bench_one_gpu_runs_the_sharded_leg():
+    line = _bench(["--gpus", "1"] + SMALL, 280)
+    assert line["n_gpus"] == 1 and line["round_trip_bit_exact"] is True
+    _check_sharded(line["sharded"], 1)
+    assert line["sharded"]["transport"].startswith("RcclTransport")

@@ -484,3 +484,87 @@ def test_mpi_rs_slices_larger_than_the_buffer(oracle, tmp_path, exchange):
         for path, size in files[r]:
             assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path
         assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[4096:], want[r]), r
+
+
+@pytest.mark.parametrize("scheme,op", [("rs", "encode"), ("rs", "rebuild")])
+def test_mpi_hang_cap_fails_the_call(oracle, tmp_path, scheme, op):
+    """The fault contract through the drop-in slot (include/redset_hip.h
+    redset_hip_hang_faults): the sharded exchange's plans forced into streamed
+    pairs (test twin, REDSET_HIP_SEQUENTIAL=3) with a loader that sleeps
+    before it publishes a job's tables and a 1-poll hang cap, so the
+    consumers' table hand-over gives up and the kernels' outputs are wrong.
+    Every member whose kernels hit the cap must return REDSET_FAILURE -- the
+    call never reports success with those bytes -- and no member may hang
+    (src/redset_reedsolomon.c:336-341). The control run with the product's
+    hang cap and the same delay succeeds and is checked like any other."""
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    tmp = str(tmp_path)
+    p, e = (4, 2) if scheme == "rs" else (4, 1)
+    d = p - e
+    rng = np.random.default_rng(21)
+    files, chunk = _setup(tmp, p, d, rng, 400_000)
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, [512] * p, reds)
+    ld = os.environ.get("LD_LIBRARY_PATH")
+    stall = {"RANK_TEST_EXCHANGE": "sharded-mpi", "REDSET_HIP_SEQUENTIAL": "3",
+             "REDSET_HIP_TEST_TABLE_DELAY": "400", "LD_LIBRARY_PATH": TWIN_DIR + (":" + ld if ld else "")}
+    args = [scheme, "encode", e, tmp, 16384]
+    if op == "rebuild":
+        res = _mpirun(p, args, env=stall)  # control: the product's hang cap
+        assert res.returncode == 0, res.stdout + res.stderr
+        lost = [0, 3] if scheme == "rs" else [1]
+        for r in lost:
+            for path, _ in files[r]:
+                os.unlink(path)
+            os.unlink(reds[r])
+        args = [scheme, "rebuild", e, tmp, 16384] + lost
+    res = _mpirun(p, args, timeout=120, env={**stall, "REDSET_HIP_TEST_HANG_CAP": "1"})
+    assert res.returncode != 0, res.stdout + res.stderr
+    assert "hit its hang cap" in res.stderr, res.stderr[-4000:]
+    assert "signal" not in res.stderr, res.stderr[-4000:]
+    if op == "encode":
+        res = _mpirun(p, args, env=stall)  # control
+        assert res.returncode == 0, res.stdout + res.stderr
+        lofi = [_logical(fl, d * chunk) for fl in files]
+        want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+        oracle.OracleRS(p, e).encode_set(lofi, want, chunk)
+        for r in range(p):
+            assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[512:], want[r]), r
+
+
+@pytest.mark.parametrize("scheme,p,e,lost", [("rs", 4, 2, [1, 3]), ("xor", 3, 1, [2])])
+def test_mpi_auto_rebuild_takes_rccl_with_a_gpu_per_member(oracle, tmp_path, scheme, p, e, lost):
+    """AUTO's production layout: members on one node, each on its
+    own GPU. The encode stays on the host ring; the rebuild must take the
+    RCCL exchange (rank_mpi.c choose_exchange) and restore the lost members
+    bit for bit. Needs >= p GPUs: the one-GPU test box skips it, a node with
+    8 GPUs runs it (src/redset_reedsolomon.c:646-733 replaced)."""
+    if not _have():
+        pytest.skip("needs a GPU, MPICH and tests/mpi/build/rank_test")
+    import torch
+
+    if torch.cuda.device_count() < p:
+        pytest.skip(f"needs {p} GPUs, one per member ({torch.cuda.device_count()} here)")
+    tmp = str(tmp_path)
+    d = p - e
+    rng = np.random.default_rng(17)
+    files, chunk = _setup(tmp, p, d, rng, 3_000_000)
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, [256] * p, reds)
+    crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
+    env = {"RANK_TEST_DEVICE_PER_RANK": "1"}
+    res = _mpirun(p, [scheme, "encode", e, tmp, 1 << 20], env=env)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "encode exchange host" in res.stdout, res.stdout
+    for r in lost:
+        for path, _ in files[r]:
+            os.unlink(path)
+        os.unlink(reds[r])
+    res = _mpirun(p, [scheme, "rebuild", e, tmp, 1 << 20] + lost, env=env)
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert "rebuild exchange rccl" in res.stdout, res.stdout
+    for r in lost:
+        for path, size in files[r]:
+            assert os.path.getsize(path) == size
+            assert oracle.crc32(np.fromfile(path, dtype=np.uint8)) == crcs[path], path

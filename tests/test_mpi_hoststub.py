@@ -211,3 +211,37 @@ def test_host_path_xor_decode_orders(stub, oracle, tmp_path, order, p, lost, buf
     # (p - 1) * p in the gather
     got = _stats(reb.stdout)["recv_bytes"][0]
     assert got == (p if order == "chain" else (p - 1) * p) * chunk, (got, chunk)
+
+
+@pytest.mark.parametrize("scheme,op,rank", [("rs", "encode", 1), ("rs", "rebuild", 3), ("xor", "encode", 0),
+                                             ("xor", "rebuild", 2)])
+def test_hang_capped_kernel_wait_fails_the_call(stub, oracle, tmp_path, scheme, op, rank):
+    """The fault contract (include/redset_hip.h redset_hip_hang_faults): when
+    the kernels' hang count moves during a backend call on one member -- a
+    wait with no fallback gave up, so that member's kernel outputs are wrong
+    -- that member's call returns REDSET_FAILURE after the collective has run
+    (no peer hangs), and the AND-reduce fails every rank
+    (src/redset_reedsolomon.c:336-341). The stub moves the count on the named
+    rank only."""
+    tmp = str(tmp_path)
+    p, e = (4, 2) if scheme == "rs" else (4, 1)
+    rng = np.random.default_rng(11)
+    files, chunk = _setup(tmp, p, p - e, rng, 200_000)
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, [512] * p, reds)
+    args = [scheme, "encode", e, tmp, 16384]
+    if op == "rebuild":
+        res = _run(p, args)
+        assert res.returncode == 0, res.stdout + res.stderr
+        lost = [1, 2] if scheme == "rs" else [2]
+        for r in lost:
+            for path, _ in files[r]:
+                os.unlink(path)
+            os.unlink(reds[r])
+        args = [scheme, "rebuild", e, tmp, 16384] + lost
+    res = _run(p, args, env={"HIPSTUB_HANG_RANK": str(rank)}, timeout=90)
+    assert res.returncode != 0, res.stdout + res.stderr
+    assert f"rank {rank}: backend failed: a kernel wait hit its hang cap" in res.stderr, res.stderr
+    others = [r for r in range(p) if r != rank]
+    assert not any(f"rank {r}: backend failed" in res.stderr for r in others), res.stderr
+    assert "signal" not in res.stderr, res.stderr

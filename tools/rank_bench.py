@@ -23,6 +23,11 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MIB = 1 << 20
 
 
+# the disjoint classes of a call's blocked host time (include/redset_hip_mpi.h)
+BLOCKED = ("read_seconds", "mpi_seconds", "gpu_seconds", "write_seconds", "stage_seconds", "copy_seconds",
+           "plan_seconds")
+
+
 def roofline(stats, p, mpi_gbps, pcie_gbps, seconds):
     """The slot's roofline for one call: per-rank bytes (max over ranks), the
     time each would take at its resource's ceiling, the share of the call
@@ -39,10 +44,13 @@ def roofline(stats, p, mpi_gbps, pcie_gbps, seconds):
     return {
         "bytes_per_rank_max": {k: int(mx[k]) for k in ("read_bytes", "sent_bytes", "recv_bytes", "h2d_bytes",
                                                           "d2h_bytes", "write_bytes")},
-        "blocked_seconds_max": {k: round(mx[k], 4) for k in ("read_seconds", "mpi_seconds", "gpu_seconds",
-                                                             "write_seconds")},
-        "blocked_seconds_mean": {k: round(mean[k], 4) for k in ("read_seconds", "mpi_seconds", "gpu_seconds",
-                                                               "write_seconds")},
+        "blocked_seconds_max": {k: round(mx.get(k, 0.0), 4) for k in BLOCKED},
+        "blocked_seconds_mean": {k: round(mean.get(k, 0.0), 4) for k in BLOCKED},
+        # the host thread's time the disjoint classes explain, summed over the
+        # ranks against the ranks' summed call time (redset_hip_rank_last_stats)
+        "blocked_coverage": round(sum(stats[k][1] for k in BLOCKED if k in stats) / stats["seconds"][1], 3),
+        "call_seconds_max": round(mx["seconds"], 4),
+        "exchange_seconds_max": round(mx.get("exchange_seconds", 0.0), 4),
         "ceilings": {"pcie_GBps_per_direction": pcie_gbps, "host_mpi_GBps_per_rank_send_plus_recv": mpi_gbps},
         "seconds_at_ceiling": {k: round(v, 4) for k, v in need.items()},
         "bound": bound,

@@ -19,9 +19,10 @@ after it as a second timed leg and reported under "sharded": N sets whose
 members are spread round-robin over the GPUs, erased members rebuilt
 column-sharded over all GPUs after an RCCL P2P gather of the decode inputs'
 slices (redset_amd.dist), exchange inside the timing, result checked bit-exact.
-The sharded leg runs at N=1 too (world-1 RCCL transport: the gather and
-return are local copies), so configs[3]'s curve has its base point in every
-N=1 line; `sharded.value` is configs[3]'s scaling number at every N.
+The sharded leg runs at N=1 too (world-1 RCCL transport: every slice is
+the process's own, computed in place, so no message moves), so configs[3]'s
+curve has its base point in every N=1 line; `sharded.value` is configs[3]'s
+scaling number at every N.
 
 Launch: under torchrun (RANK / WORLD_SIZE set) every process is one rank.
 `--gpus N > 1` without torchrun starts the N ranks itself, as a torchrun child
@@ -410,8 +411,8 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     their hosts. Parity comes from one untimed sharded encode beforehand.
     After timing every GPU checks that its lost members' slabs are back bit
     for bit (min over ranks). At world 1 (no process group) the transport is
-    RCCL over a one-rank communicator: gather and return are local copies
-    and the step is configs[3]'s N=1 point."""
+    RCCL over a one-rank communicator with nothing to send, and the step is
+    configs[3]'s N=1 point."""
     import torch
     import torch.distributed as dist
 
@@ -455,18 +456,17 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     # xGMI mesh: one link per peer pair, world - 1 links usable per GPU).
     link_peak = (world - 1) * XGMI_LINK_GBPS
     fabric_gbps = sent_mean / s_step / 1e9
-    local_bytes = int(runner.info("rebuild")["local_bytes"])
     out = {
         "workload": (f"{world} sets of p={p} (RS({p - e}+{e}), chunk {chunk / MIB:g} MiB), members round-robin over "
                      f"{world} GPUs; rebuild of members {lost} of every set, column-sharded (BASELINE.json configs[3])"),
         "value": round(value, 2),
         "unit": "GB/s",
         # north_star: the sharded rebuild "as absolute GB/s and as fraction of HBM peak"
-        "frac_of_hbm": round(value / (world * HBM_PEAK_GBPS), 4),
+        "frac_of_hbm": round(value / (world * HBM_PEAK_GBPS), 6),
         "hbm_peak_GBps": world * HBM_PEAK_GBPS,
         "ms_per_step": round(s_step * 1e3, 4),
         "bit_exact": bool(ok),
-        "transport": type(runner._transport).__name__ + ("" if dist_on else " (world 1: local copies)"),
+        "transport": type(runner._transport).__name__ + ("" if dist_on else " (world 1: no messages)"),
         "schedule": "sets pipelined: set k+1's gather overlaps set k's gf_mac (redset_hip_sharded_execute)",
         "pipelined_event_ms_rank0": pipelined_event_ms,
         "roofline": {
@@ -480,15 +480,14 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
                             "GPU pair of the node's fully connected mesh, 7 per GPU at 8 GPUs (SURVEY.md §5; "
                             "MI355X platform figure, not measured here)"),
         } if dist_on else {
-            # world 1: nothing crosses the fabric; the step is HBM-bound --
-            # the gather's and return's local copies (read + write) plus the
-            # gf_mac's own algorithmic bytes
+            # world 1: nothing crosses the fabric and nothing is copied (a
+            # process computes its own slice of the members it hosts in
+            # place): the step is the gf_mac's, HBM-bound
             "bound": "hbm",
-            "achieved": round((2 * local_bytes + runner.algorithmic_bytes("rebuild")) / s_step / 1e9, 1),
+            "achieved": round(runner.algorithmic_bytes("rebuild") / s_step / 1e9, 1),
             "peak": HBM_PEAK_GBPS,
-            "unit": "GB/s (HBM bytes of copies + gf_mac / step time)",
-            "frac": round((2 * local_bytes + runner.algorithmic_bytes("rebuild")) / s_step / 1e9 / HBM_PEAK_GBPS, 4),
-            "local_copy_bytes_per_step": local_bytes,
+            "unit": "GB/s (algorithmic bytes / step time)",
+            "frac": round(runner.algorithmic_bytes("rebuild") / s_step / 1e9 / HBM_PEAK_GBPS, 4),
         },
         # HBM is the bound of the compute phase alone (phased diagnostic)
         "compute_hbm": {
@@ -506,13 +505,31 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
 
 _PRINT_LOCK = threading.Lock()
 _PRINTED = threading.Event()
+_RESULT_OUT = None
+
+
+def claim_stdout():
+    """Keep stdout for the one JSON line: the process's fd 1 goes to stderr
+    from here on (RCCL prints a version banner to stdout when a communicator
+    is created, on every rank), and the line is written to a duplicate of
+    the original stdout."""
+    global _RESULT_OUT
+    sys.stdout.flush()
+    fd = os.dup(1)
+    os.dup2(2, 1)
+    _RESULT_OUT = os.fdopen(fd, "w", buffering=1)
+
+
+def _print_result(result):
+    out = _RESULT_OUT or sys.stdout
+    print(json.dumps(result), file=out, flush=True)
 
 
 def emit(result, rank):
     """Rank 0 prints the one JSON line (once, whichever thread gets here first)."""
     with _PRINT_LOCK:
         if rank == 0 and not _PRINTED.is_set():
-            print(json.dumps(result), flush=True)
+            _print_result(result)
         _PRINTED.set()
 
 
@@ -528,7 +545,7 @@ def sharded_expired(result, rank, limit):
         if not _PRINTED.is_set():
             result["sharded"] = {"error": f"timed out after {limit:g} s"}
             if rank == 0:
-                print(json.dumps(result), flush=True)
+                _print_result(result)
             _PRINTED.set()
         print(f"rank {rank}: sharded leg or final barrier timed out after {limit:g} s", file=sys.stderr, flush=True)
         os._exit(WATCHDOG_EXIT)
@@ -590,12 +607,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world == 1 and args.gpus > 1 and "RANK" not in os.environ:
         sys.exit(self_launch(sys.argv[1:], args.gpus, args.launch_timeout))
+    claim_stdout()
     import torch
 
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
-        print(json.dumps({"error": f"--gpus {args.gpus} but WORLD_SIZE={world}"}))
+        _print_result({"error": f"--gpus {args.gpus} but WORLD_SIZE={world}"})
         sys.exit(2)
     dev = local_rank % max(1, torch.cuda.device_count())
     torch.cuda.set_device(dev)

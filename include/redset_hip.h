@@ -314,7 +314,7 @@ typedef struct {
   unsigned long long gather_bytes_recv;
   unsigned long long return_bytes_sent;
   unsigned long long return_bytes_recv;
-  unsigned long long local_bytes;         /* copied within this process */
+  unsigned long long local_bytes;         /* copied within this process: 0 (own slices computed in place) */
   unsigned long long compute_bytes;       /* algorithmic bytes of this process's slice */
   unsigned long long gather_msg_max;      /* largest / smallest peer message this process sends */
   unsigned long long gather_msg_min;

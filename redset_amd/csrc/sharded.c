@@ -62,12 +62,12 @@ static int xl_push(xlist* L, redset_hip_xfer x) {
  * Both processes of a pair walk the same rows in the same order, and a row's
  * offset on one side differs from its offset on the other by a constant of
  * the pair (the buffers share one layout), so they merge alike and the
- * message lengths match. Local copies keep (src, dst) pairs. */
+ * message lengths match. Nothing moves within a process: its own slice of
+ * the members it hosts is computed in place (plan_sets). */
 typedef struct {
   int world, rank;
   xlist* send;   /* [world] */
   xlist* recv;   /* [world] */
-  xlist copy;    /* src, dst, src, dst, ... */
 } exch;
 
 static int ex_init(exch* X, int world, int rank) {
@@ -84,7 +84,6 @@ static void ex_free(exch* X) {
   for (int g = 0; X->recv && g < X->world; ++g) free(X->recv[g].v);
   free(X->send);
   free(X->recv);
-  free(X->copy.v);
   memset(X, 0, sizeof(*X));
 }
 
@@ -103,36 +102,15 @@ static int ex_row(xlist* L, int peer, int send, unsigned char* buf, size_t len) 
 static int ex_send(exch* X, int peer, unsigned char* buf, size_t len) { return ex_row(&X->send[peer], peer, 1, buf, len); }
 static int ex_recv(exch* X, int peer, unsigned char* buf, size_t len) { return ex_row(&X->recv[peer], peer, 0, buf, len); }
 
-static int ex_copy(exch* X, unsigned char* dst, const unsigned char* src, size_t len) {
-  xlist* L = &X->copy;
-  if (L->n >= 2) {
-    redset_hip_xfer* s = &L->v[L->n - 2];
-    redset_hip_xfer* d = &L->v[L->n - 1];
-    if ((const unsigned char*) s->buf + s->len == src && (unsigned char*) d->buf + d->len == dst) {
-      s->len += len;
-      d->len += len;
-      return 0;
-    }
-  }
-  redset_hip_xfer a = {X->rank, 1, (void*) src, len};
-  redset_hip_xfer b = {X->rank, 0, dst, len};
-  int rc = xl_push(L, a);
-  return rc ? rc : xl_push(L, b);
-}
-
 /* message statistics of one phase (the info block) */
 typedef struct {
   int *messages, *recv_messages;
-  unsigned long long *sent, *recvd, *local, *max_msg, *min_msg;
+  unsigned long long *sent, *recvd, *max_msg, *min_msg;
 } xstats;
 
-/* flatten into one list for the transport: local copies, then per peer its
- * sends and receives; byte counts and message sizes for the info block */
+/* flatten into one list for the transport: per peer its sends and
+ * receives; byte counts and message sizes for the info block */
 static int ex_flatten(exch* X, xlist* out, const xstats* st) {
-  for (int i = 0; i < X->copy.n; ++i) {
-    if (xl_push(out, X->copy.v[i])) return REDSET_FAILURE;
-    if (X->copy.v[i].send) *st->local += X->copy.v[i].len;
-  }
   for (int g = 0; g < X->world; ++g) {
     for (int i = 0; i < X->send[g].n; ++i) {
       const unsigned long long len = X->send[g].v[i].len;
@@ -263,24 +241,24 @@ static int wanted(const pctx* C, int r, int pass, int x) {
 
 /* set k's gather: slice g of every needed cell of every surviving member of
  * the set goes from its host to process g; data rows then parity rows,
- * members in slot order (both ends of a pair walk the same rows) */
+ * members in slot order (both ends of a pair walk the same rows). My own
+ * slice of the members I host stays where it is: the compute reads it in
+ * the hosted slabs (plan_sets), so nothing is copied within the process */
 static int plan_gather(const pctx* C, int k, exch* G) {
   const int me = C->me;
   int rc = 0;
   for (int g = 0; g < C->world && !rc; ++g) {
+    if (g == me) continue;
     for (int pass = 0; pass < 2 && !rc; ++pass) {
       const int ncell = pass == 0 ? C->d : C->e;
-      for (int j = 0; j < C->mh && !rc; ++j) { /* what I send to g (g == me: copy) */
+      for (int j = 0; j < C->mh && !rc; ++j) { /* what I send to g */
         const int m = C->by_slot[(size_t) me * C->mh + j];
         if (m < 0 || m / C->p != k) continue;
         for (int x = 0; x < ncell && !rc; ++x) {
           if (!wanted(C, m % C->p, pass, x)) continue;
-          unsigned char* src = pass == 0 ? hd(C, g, j, x) : hp(C, g, j, x);
-          if (g == me) rc = ex_copy(G, pass == 0 ? gd(C, me, j, x) : gp(C, me, j, x), src, C->W);
-          else rc = ex_send(G, g, src, C->W);
+          rc = ex_send(G, g, pass == 0 ? hd(C, g, j, x) : hp(C, g, j, x), C->W);
         }
       }
-      if (g == me) continue;
       for (int j = 0; j < C->mh && !rc; ++j) { /* my slice of g's members' needed cells */
         const int m = C->by_slot[(size_t) g * C->mh + j];
         if (m < 0 || m / C->p != k) continue;
@@ -294,7 +272,8 @@ static int plan_gather(const pctx* C, int k, exch* G) {
 
 /* set k's return: the outputs (encode: every member's parity; rebuild: every
  * cell of the lost members) go from each process's gathered slots to the
- * member's host: data rows, then parity rows, members in set order */
+ * member's host: data rows, then parity rows, members in set order. A
+ * member I host got my slice in place (the compute wrote its hosted slab) */
 static int plan_return(const pctx* C, int k, exch* R) {
   int rc = 0;
   for (int pass = 0; pass < 2 && !rc; ++pass) {
@@ -305,15 +284,12 @@ static int plan_return(const pctx* C, int k, exch* R) {
       if (!is_out) continue;
       const int h = C->L->host[m], j = C->L->slot[m];
       const size_t len = (size_t) (pass == 0 ? C->d : C->e) * C->W;
-      unsigned char* mine = pass == 0 ? gd(C, h, j, 0) : gp(C, h, j, 0);
       if (h != C->me) {
-        rc = ex_send(R, h, mine, len);
+        rc = ex_send(R, h, pass == 0 ? gd(C, h, j, 0) : gp(C, h, j, 0), len);
         continue;
       }
-      for (int g = 0; g < C->world && !rc; ++g) {
-        unsigned char* dst = pass == 0 ? hd(C, g, j, 0) : hp(C, g, j, 0);
-        rc = g == C->me ? ex_copy(R, dst, mine, len) : ex_recv(R, g, dst, len);
-      }
+      for (int g = 0; g < C->world && !rc; ++g)
+        if (g != C->me) rc = ex_recv(R, g, pass == 0 ? hd(C, g, j, 0) : hp(C, g, j, 0), len);
     }
   }
   return rc;
@@ -396,11 +372,9 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
   for (int k = 0; k < L->nsets && !rc; ++k) {
     rc = plan_gather(&C, k, &G);
     const xstats gs = {&P->info.gather_messages, &P->info.gather_recv_messages, &P->info.gather_bytes_sent,
-                       &P->info.gather_bytes_recv, &P->info.local_bytes, &P->info.gather_msg_max,
-                       &P->info.gather_msg_min};
+                       &P->info.gather_bytes_recv, &P->info.gather_msg_max, &P->info.gather_msg_min};
     const xstats rs_ = {&P->info.return_messages, &P->info.return_recv_messages, &P->info.return_bytes_sent,
-                        &P->info.return_bytes_recv, &P->info.local_bytes, &P->info.return_msg_max,
-                        &P->info.return_msg_min};
+                        &P->info.return_bytes_recv, &P->info.return_msg_max, &P->info.return_msg_min};
     if (!rc) rc = ex_flatten(&G, &P->gather, &gs);
     if (!rc) rc = plan_return(&C, k, &R);
     if (!rc) rc = ex_flatten(&R, &P->ret, &rs_);
@@ -413,7 +387,9 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
   }
   if (rc) goto done;
 
-  /* compute: every set over my slices in the gathered layout (cell stride W) */
+  /* compute: every set over my slices, cell stride W: a member hosted
+   * elsewhere in the gathered layout, a member I host in place in its
+   * hosted slabs (my slice q = me is [d][W] / [e][W] there too) */
   P->plans = calloc((size_t) L->nsets, sizeof(*P->plans));
   P->lofi = malloc(sizeof(*P->lofi) * (size_t) nm);
   P->parity = malloc(sizeof(*P->parity) * (size_t) nm);
@@ -422,8 +398,9 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
     goto done;
   }
   for (int m = 0; m < nm; ++m) {
-    P->lofi[m] = gd(&C, L->host[m], L->slot[m], 0);
-    P->parity[m] = gp(&C, L->host[m], L->slot[m], 0);
+    const int local = L->host[m] == me;
+    P->lofi[m] = local ? hd(&C, me, L->slot[m], 0) : gd(&C, L->host[m], L->slot[m], 0);
+    P->parity[m] = local ? hp(&C, me, L->slot[m], 0) : gp(&C, L->host[m], L->slot[m], 0);
   }
   const size_t n = P->info.my_slice_len;
   P->info.compute_bytes = (unsigned long long) L->nsets * p * (d + (is_encode(kind) ? e : missing)) * n;

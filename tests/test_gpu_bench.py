@@ -41,7 +41,7 @@ def _bench(args, timeout):
 def _check_sharded(sh, world):
     assert "error" not in sh, sh
     assert sh["bit_exact"] is True
-    assert sh["value"] > 0 and 0 < sh["frac_of_hbm"] < 1
+    assert sh["value"] > 0 and 0 < sh["frac_of_hbm"] < 1  # gloo moves tens of MB/s: a tiny fraction
     assert sh["hbm_peak_GBps"] == world * 8000.0
     msgs = sh["exchange"]["messages_per_gpu"]["rebuild"]
     if world > 1:
@@ -50,7 +50,7 @@ def _check_sharded(sh, world):
         assert sh["exchange"]["bytes_sent_per_gpu_per_step"] > 0
     else:
         assert msgs["gather_messages"] == 0 and msgs["return_messages"] == 0, msgs
-        assert sh["roofline"]["bound"] == "hbm" and sh["roofline"]["local_copy_bytes_per_step"] > 0
+        assert sh["roofline"]["bound"] == "hbm" and sh["exchange"]["bytes_sent_per_gpu_per_step"] == 0
 
 
 @pytest.mark.timeout(420)

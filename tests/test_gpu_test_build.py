@@ -66,7 +66,9 @@ def _child(tmp_path, name, extra_env, args, timeout):
             [sys.executable, "-u", "-m", "pytest", os.path.join(ROOT, "tests"), "-x", "-v",
              "-p", "no:cacheprovider", "--timeout", "300", "--timeout-method", "thread",
              "--deselect", f"{SELF}::test_gpu_suite_bit_exact_with_ring_fallbacks",
-             "--deselect", f"{SELF}::test_knob_tests_with_the_normal_ring"] + args,
+             "--deselect", f"{SELF}::test_knob_tests_with_the_normal_ring",
+             # bench.py end to end is the product's; its kernels run in this suite anyway
+             "--ignore", os.path.join(ROOT, "tests", "test_gpu_bench.py")] + args,
             cwd=ROOT, env=env, stdout=f, stderr=subprocess.STDOUT, text=True, timeout=timeout)
     with open(child_log) as f:
         text = f.read()

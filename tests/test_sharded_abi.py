@@ -151,7 +151,7 @@ def test_world1_plan_with_callbacks_matches_oracle(L, oracle, p, e, chunk, lost)
             assert np.array_equal(HP[0, slot[k * p + r], :, :chunk].reshape(-1), par[r]), (k, r)
     info = L.ShardedInfo()
     assert lib.redset_hip_sharded_get_info(reb, ctypes.byref(info)) == 0
-    assert info.gather_bytes_sent == 0 and info.gather_messages == 0 and info.local_bytes > 0
+    assert info.gather_bytes_sent == 0 and info.gather_messages == 0 and info.local_bytes == 0
     for k in range(nsets):
         for r in lost:
             HD[0, slot[k * p + r]] = 0xEE

@@ -29,7 +29,7 @@ s=$?; echo "bench exit $s" | tee -a "$OUT/progress.txt"; head -c 600 "$OUT/bench
 [ -n "$NO_PROF" ] && { echo "== done (no profiles)" | tee -a "$OUT/progress.txt"; exit 0; }
 echo "== rocprofv3 kernel stats" | tee -a "$OUT/progress.txt"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/prof" -o bench -- \
-  python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --pairs 0 > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
+  python3 bench.py --steps 20 --warmup 5 --cpu-baseline 0 --pairs 0 --sharded 0 > "$OUT/prof_bench.json" 2> "$OUT/prof.err"
 s=$?; echo "rocprof exit $s" | tee -a "$OUT/progress.txt"; ok $s || exit $s
 echo "== rocprofv3 PMC FETCH_SIZE / WRITE_SIZE (separate passes)" | tee -a "$OUT/progress.txt"
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d "$OUT/pmc_fetch" -o fetch -- \

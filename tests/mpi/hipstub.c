@@ -90,3 +90,127 @@ int redset_hip_hang_faults(void* s, unsigned* count, int clear) {
   *count = (want && me && atoi(want) == atoi(me)) ? reads++ : 0;
   return 0;
 }
+
+/* ---- whole-set plans, on the CPU ------------------------------------------
+ * The sharded exchange (sharded.c, inside libredset_hip.so) computes each
+ * set through redset_hip_{rs,xor}_plan_* + redset_hip_plan_execute, which
+ * launch kernels. These stand-ins keep the plan's pointers and run the same
+ * arithmetic on the CPU at execute, so the per-rank backends' sharded slot
+ * (rank_mpi.c sharded_slot: windows, planning, staging, exchanges) runs here
+ * too. The layout maps and decode maps come from the library itself
+ * (redset_hip_rs_get_encoding_id / _get_data_id / _rs_matrix /
+ * _rs_decode_matrix); the bytes are checked against the oracle by the tests. */
+typedef struct redset_hip_rs redset_hip_rs;
+int redset_hip_rs_shape(const redset_hip_rs* rs, int* ranks, int* encoding);
+int redset_hip_rs_matrix(const redset_hip_rs* rs, unsigned char* mat_out);
+int redset_hip_rs_get_encoding_id(int ranks, int encoding, int rank, int chunk_id);
+int redset_hip_rs_get_data_id(int ranks, int encoding, int rank, int chunk_id);
+int redset_hip_rs_decode_matrix(const redset_hip_rs* rs, int missing, const int* rebuild_ranks, int chunk_id,
+                                unsigned char* coef_out);
+
+enum { STUB_RS_ENCODE = 1, STUB_RS_REBUILD = 2, STUB_XOR_ENCODE = 3, STUB_XOR_REBUILD = 4 };
+struct redset_hip_plan {
+  int kind, p, e, missing, lost[256];
+  const redset_hip_rs* rs;
+  unsigned char **lofi, **par;
+  size_t n, stride;
+};
+
+static int stub_plan(int kind, const redset_hip_rs* rs, int p, int e, int missing, const int* lost,
+                     unsigned char* const* lofi, unsigned char* const* par, size_t n, size_t stride,
+                     struct redset_hip_plan** out) {
+  struct redset_hip_plan* P = calloc(1, sizeof(*P));
+  if (!P) return 1;
+  P->kind = kind, P->rs = rs, P->p = p, P->e = e, P->missing = missing, P->n = n, P->stride = stride;
+  for (int i = 0; i < missing; ++i) P->lost[i] = lost[i];
+  P->lofi = malloc(sizeof(*P->lofi) * (size_t) p);
+  P->par = malloc(sizeof(*P->par) * (size_t) p);
+  for (int r = 0; r < p; ++r) P->lofi[r] = lofi[r], P->par[r] = par[r];
+  *out = P;
+  return 0;
+}
+
+int redset_hip_rs_plan_encode(const redset_hip_rs* rs, unsigned char* const* lofi, unsigned char* const* parity,
+                              size_t chunk, size_t stride, struct redset_hip_plan** out) {
+  int p, e;
+  redset_hip_rs_shape(rs, &p, &e);
+  return stub_plan(STUB_RS_ENCODE, rs, p, e, 0, NULL, lofi, parity, chunk, stride, out);
+}
+int redset_hip_rs_plan_rebuild(const redset_hip_rs* rs, int missing, const int* lost, unsigned char* const* lofi,
+                               unsigned char* const* parity, size_t chunk, size_t stride,
+                               struct redset_hip_plan** out) {
+  int p, e;
+  redset_hip_rs_shape(rs, &p, &e);
+  return stub_plan(STUB_RS_REBUILD, rs, p, e, missing, lost, lofi, parity, chunk, stride, out);
+}
+int redset_hip_xor_plan_encode(int p, unsigned char* const* lofi, unsigned char* const* xorc, size_t chunk,
+                               size_t stride, struct redset_hip_plan** out) {
+  return stub_plan(STUB_XOR_ENCODE, NULL, p, 1, 0, NULL, lofi, xorc, chunk, stride, out);
+}
+int redset_hip_xor_plan_rebuild(int p, int root, unsigned char* const* lofi, unsigned char* const* xorc,
+                                size_t chunk, size_t stride, struct redset_hip_plan** out) {
+  return stub_plan(STUB_XOR_REBUILD, NULL, p, 1, 1, &root, lofi, xorc, chunk, stride, out);
+}
+void redset_hip_plan_destroy(struct redset_hip_plan* P) {
+  if (!P) return;
+  free(P->lofi);
+  free(P->par);
+  free(P);
+}
+
+/* member r's cell of stripe c (src/redset_reedsolomon_common.c:822-853;
+ * XOR: src/redset_xor.c:251-266) */
+static unsigned char* stub_cell(const struct redset_hip_plan* P, int r, int c) {
+  if (P->kind >= STUB_XOR_ENCODE) return c == r ? P->par[r] : P->lofi[r] + (size_t) (c < r ? c : c - 1) * P->stride;
+  const int enc = redset_hip_rs_get_encoding_id(P->p, P->e, r, c);
+  return enc < P->p ? P->lofi[r] + (size_t) redset_hip_rs_get_data_id(P->p, P->e, r, c) * P->stride
+                    : P->par[r] + (size_t) (enc - P->p) * P->stride;
+}
+
+int redset_hip_plan_execute(const struct redset_hip_plan* P, void* stream) {
+  (void) stream;
+  const int p = P->p, e = P->e;
+  unsigned char* mat = malloc((size_t) (p + e) * p);
+  unsigned char* D = malloc((size_t) (P->missing ? P->missing : 1) * p);
+  if (P->rs && P->kind == STUB_RS_ENCODE) redset_hip_rs_matrix(P->rs, mat);
+  for (int c = 0; c < p; ++c) {
+    if (P->kind == STUB_RS_ENCODE) { /* parity slot i of stripe c = row p + i over its data holders */
+      for (int r = 0; r < p; ++r) {
+        const int enc = redset_hip_rs_get_encoding_id(p, e, r, c);
+        if (enc < p) continue;
+        unsigned char* out = stub_cell(P, r, c);
+        memset(out, 0, P->n);
+        for (int s = 0; s < p; ++s) {
+          if (redset_hip_rs_get_encoding_id(p, e, s, c) >= p) continue;
+          const uint8_t k = mat[(size_t) enc * p + s];
+          const unsigned char* in = stub_cell(P, s, c);
+          for (size_t b = 0; b < P->n; ++b) out[b] ^= gf_mul(k, in[b]);
+        }
+      }
+    } else if (P->kind == STUB_RS_REBUILD) {
+      redset_hip_rs_decode_matrix(P->rs, P->missing, P->lost, c, D);
+      for (int i = 0; i < P->missing; ++i) {
+        unsigned char* out = stub_cell(P, P->lost[i], c);
+        memset(out, 0, P->n);
+        for (int s = 0; s < p; ++s) {
+          const uint8_t k = D[(size_t) i * p + s];
+          if (!k) continue;
+          const unsigned char* in = stub_cell(P, s, c);
+          for (size_t b = 0; b < P->n; ++b) out[b] ^= gf_mul(k, in[b]);
+        }
+      }
+    } else { /* XOR: the target of stripe c is member c's chunk (encode) or the root's cell */
+      const int t = P->kind == STUB_XOR_ENCODE ? c : P->lost[0];
+      unsigned char* out = stub_cell(P, t, c);
+      memset(out, 0, P->n);
+      for (int s = 0; s < p; ++s) {
+        if (s == t) continue;
+        const unsigned char* in = stub_cell(P, s, c);
+        for (size_t b = 0; b < P->n; ++b) out[b] ^= in[b];
+      }
+    }
+  }
+  free(mat);
+  free(D);
+  return 0;
+}

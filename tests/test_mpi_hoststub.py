@@ -84,7 +84,7 @@ def _round_trip(oracle, tmp, scheme, p, e, lost, buf, seed, maxsize, header=None
         os.unlink(reds[r])
     res = _run(p, [scheme, "rebuild", e, tmp, buf] + lost, env=env)
     assert res.returncode == 0, res.stdout + res.stderr
-    assert "rebuild exchange host" in res.stdout, res.stdout
+    assert f"rebuild exchange {(env or {}).get('RANK_TEST_EXCHANGE', 'host')}" in res.stdout, res.stdout
     for r in lost:
         for path, size in files[r]:
             assert os.path.getsize(path) == size
@@ -245,3 +245,34 @@ def test_hang_capped_kernel_wait_fails_the_call(stub, oracle, tmp_path, scheme, 
     others = [r for r in range(p) if r != rank]
     assert not any(f"rank {r}: backend failed" in res.stderr for r in others), res.stderr
     assert "signal" not in res.stderr, res.stderr
+
+
+TWIN_DIR = os.path.join(ROOT, "redset_amd", "lib_test")
+
+
+@pytest.mark.parametrize("scheme,p,e,lost,window", [("rs", 6, 2, [1, 4], 0), ("rs", 5, 3, [0, 2, 4], 0),
+                                                     ("xor", 4, 1, [2], 0), ("rs", 4, 2, [0, 3], 65536),
+                                                     ("xor", 5, 1, [0], 40000)])
+def test_sharded_slot_round_trip(stub, oracle, tmp_path, scheme, p, e, lost, window):
+    """The per-rank backends' sharded exchange (rank_mpi.c sharded_slot: the
+    RCCL path's plan, here over the MPI transport with device buffers) on the
+    CPU: the HIP stand-in also runs the whole-set plans the sharded plan
+    computes with, so the slot's windows, planning, transport reserve,
+    staging and exchanges run end to end, encode and rebuild, checked against
+    the oracle. window > 0: the test twin with windows of that many bytes, so
+    a set takes several (double-buffered, a tail window)."""
+    env = {"RANK_TEST_EXCHANGE": "sharded-mpi", "RANK_TEST_REPEAT": "2"}
+    if window:
+        env["REDSET_HIP_TEST_SHARDED_WINDOW"] = str(window)
+        env["LD_LIBRARY_PATH"] = TWIN_DIR + (":" + os.environ["LD_LIBRARY_PATH"] if os.environ.get("LD_LIBRARY_PATH")
+                                               else "")
+    enc, reb, chunk = _round_trip(oracle, str(tmp_path), scheme, p, e, lost, 32768, 900 + p, 300_000, env=env)
+    assert "encode exchange sharded-mpi" in enc.stdout, enc.stdout
+    for res in (enc, reb):
+        st = _stats(res.stdout, "warm")
+        classes = ["read_seconds", "mpi_seconds", "gpu_seconds", "write_seconds", "stage_seconds", "copy_seconds",
+                   "plan_seconds"]
+        # the disjoint classes never exceed the call (per rank: compare sums)
+        assert sum(st[k][1] for k in classes) <= st["seconds"][1] * 1.0001, st
+        assert st["exchange_seconds"][0] > 0 and st["plan_seconds"][0] > 0, st
+        assert st["sent_bytes"][1] == st["recv_bytes"][1] > 0, st

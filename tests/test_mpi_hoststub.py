@@ -213,9 +213,10 @@ def test_host_path_xor_decode_orders(stub, oracle, tmp_path, order, p, lost, buf
     assert got == (p if order == "chain" else (p - 1) * p) * chunk, (got, chunk)
 
 
+@pytest.mark.parametrize("exchange", ["host", "sharded-mpi"])
 @pytest.mark.parametrize("scheme,op,rank", [("rs", "encode", 1), ("rs", "rebuild", 3), ("xor", "encode", 0),
                                              ("xor", "rebuild", 2)])
-def test_hang_capped_kernel_wait_fails_the_call(stub, oracle, tmp_path, scheme, op, rank):
+def test_hang_capped_kernel_wait_fails_the_call(stub, oracle, tmp_path, scheme, op, rank, exchange):
     """The fault contract (include/redset_hip.h redset_hip_hang_faults): when
     the kernels' hang count moves during a backend call on one member -- a
     wait with no fallback gave up, so that member's kernel outputs are wrong
@@ -239,8 +240,9 @@ def test_hang_capped_kernel_wait_fails_the_call(stub, oracle, tmp_path, scheme, 
                 os.unlink(path)
             os.unlink(reds[r])
         args = [scheme, "rebuild", e, tmp, 16384] + lost
-    res = _run(p, args, env={"HIPSTUB_HANG_RANK": str(rank)}, timeout=90)
+    res = _run(p, args, env={"HIPSTUB_HANG_RANK": str(rank), "RANK_TEST_EXCHANGE": exchange}, timeout=90)
     assert res.returncode != 0, res.stdout + res.stderr
+    assert f"{op} exchange {exchange}" in res.stdout, res.stdout
     assert f"rank {rank}: backend failed: a kernel wait hit its hang cap" in res.stderr, res.stderr
     others = [r for r in range(p) if r != rank]
     assert not any(f"rank {r}: backend failed" in res.stderr for r in others), res.stderr

@@ -77,3 +77,19 @@ def test_self_launch_relays_child_line_and_status(tmp_path):
     assert "printed no result line" in out[1] and "printed no result line" in out[2]
     assert out[3] == "rcs 0 1 -9"
     assert "rank log" in r.stderr
+
+
+def test_claimed_stdout_carries_only_the_result_line():
+    """RCCL prints a version banner to stdout (C stdio) when a communicator is
+    created; after claim_stdout() anything written to fd 1 -- C printf or
+    Python print -- goes to stderr, and only the result line to stdout."""
+    r = _run("import bench, ctypes\n"
+             "bench.claim_stdout()\n"
+             "libc = ctypes.CDLL(None)\n"
+             "libc.printf(b'RCCL version : banner\\n')\n"
+             "libc.fflush(None)\n"
+             "print('a stray python print')\n"
+             "bench.emit({'metric': 'm', 'value': 7.0}, 0)\n")
+    assert r.returncode == 0, r.stderr
+    assert r.stdout.strip().splitlines() == ['{"metric": "m", "value": 7.0}'], r.stdout
+    assert "RCCL version" in r.stderr and "stray" in r.stderr

@@ -98,6 +98,10 @@ int redset_hip_rank_last_exchange(void);
  *                          through pinned memory (D2H / H2D copies, waited)
  *   copy_seconds           enqueueing the sharded windows' H2D / D2H copies
  *   plan_seconds           planning the sharded exchanges
+ *   setup_seconds          the call's own resources: choosing the exchange
+ *                          (and creating / destroying a _SHARDED_MPI
+ *                          transport), scratch buffers and stream from the
+ *                          cache or new, events, tearing the plans down
  * exchange_seconds is the host time inside redset_hip_sharded_execute (the
  * sharded calls' exchanges and kernels; it contains their mpi, gpu and stage
  * time and is not one of the classes). */
@@ -105,7 +109,7 @@ typedef struct {
   double seconds;
   double read_seconds, mpi_seconds, gpu_seconds, write_seconds;
   unsigned long long read_bytes, sent_bytes, recv_bytes, h2d_bytes, d2h_bytes, write_bytes;
-  double stage_seconds, copy_seconds, plan_seconds, exchange_seconds;
+  double stage_seconds, copy_seconds, plan_seconds, exchange_seconds, setup_seconds;
 } redset_hip_rank_stats;
 int redset_hip_rank_last_stats(redset_hip_rank_stats* out);
 

@@ -207,6 +207,7 @@ typedef struct {
 } scratch;
 
 static void scratch_init(scratch* S) {
+  const double t0 = now_s();
   memset(S, 0, sizeof(*S));
   S->device = current_device();
   if (cache_on()) {
@@ -221,10 +222,18 @@ static void scratch_init(scratch* S) {
     S->stream = NULL;
     S->rc = fail("hipStreamCreate failed");
   }
+  g_stats.setup_seconds += now_s() - t0;
 }
 
 /* the smallest cached buffer of the kind that holds n bytes, or a new one */
+static uint8_t* scratch_take(scratch* S, size_t n, int dev);
 static uint8_t* scratch_get(scratch* S, size_t n, int dev) {
+  const double t0 = now_s();
+  uint8_t* p = scratch_take(S, n, dev);
+  g_stats.setup_seconds += now_s() - t0;
+  return p;
+}
+static uint8_t* scratch_take(scratch* S, size_t n, int dev) {
   void* p = NULL;
   if (S->rc || S->nbuf == 2 * MAX_SCRATCH) return NULL;
   if (n == 0) n = 1;
@@ -267,7 +276,13 @@ static void release(const pooled* b) {
 }
 
 /* ok: the call succeeded, its scratch may be cached */
+static void scratch_release(scratch* S, int ok);
 static void scratch_free(scratch* S, int ok) {
+  const double t0 = now_s();
+  scratch_release(S, ok);
+  g_stats.setup_seconds += now_s() - t0;
+}
+static void scratch_release(scratch* S, int ok) {
   if (S->stream && hipStreamSynchronize(S->stream) != hipSuccess) ok = 0;
   ok = ok && cache_on();
   pthread_mutex_lock(&pool_mu);
@@ -1211,8 +1226,23 @@ static int rccl_create(MPI_Comm comm, int p, int r, comm_exchange* X) {
  * not yet run on a node with a GPU per member; forcing
  * _SHARDED_RCCL still sends an encode there. *tr is set for the sharded
  * modes; *mpi_t is a transport to destroy after the call (SHARDED_MPI). */
+static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, redset_hip_transport* tr,
+                               redset_hip_mpi_transport** mpi_t);
 static int choose_exchange(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, redset_hip_transport* tr,
                            redset_hip_mpi_transport** mpi_t) {
+  const double t0 = now_s();
+  const int rc = choose_exchange_now(comm, p, r, auto_rccl, mode, tr, mpi_t);
+  g_stats.setup_seconds += now_s() - t0;
+  return rc;
+}
+/* the transport of a _SHARDED_MPI call, destroyed after it (its pinned staging goes too) */
+static void transport_done(redset_hip_mpi_transport* mt) {
+  const double t0 = now_s();
+  redset_hip_mpi_transport_destroy(mt);
+  g_stats.setup_seconds += now_s() - t0;
+}
+static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, redset_hip_transport* tr,
+                               redset_hip_mpi_transport** mpi_t) {
   int m[2] = {g_exchange_mode, -g_exchange_mode}, mm[2];
   *mpi_t = NULL;
   if (MPI_Allreduce(m, mm, 2, MPI_INT, MPI_MAX, comm) != MPI_SUCCESS) return fail("MPI_Allreduce failed");
@@ -1299,8 +1329,10 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
   redset_hip_sharded* plan[2][2] = {{NULL, NULL}, {NULL, NULL}}; /* [buffer][tail window] */
   hipEvent_t ev[2] = {NULL, NULL};
   int rc = S.rc ? S.rc : hrc;
+  const double te = now_s();
   for (int k = 0; k < 2 && !rc; ++k)
     if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
+  g_stats.setup_seconds += now_s() - te;
   if (!rc && (!want || !D || !host || !slot)) rc = fail("out of host memory");
   if (!rc && need_rebuild && !lofi->write) rc = fail("lofi has no write callback");
   /* which of my cells the exchange reads: the encode every data cell, the
@@ -1436,13 +1468,15 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
     }
   }
   (void) stopped;
-out:
+out:;
+  const double tt = now_s();
   if (S.stream) (void) hipStreamSynchronize(S.stream);
   for (int b = 0; b < 2; ++b)
     for (int t = 0; t < 2; ++t) redset_hip_sharded_destroy(plan[b][t]);
-  scratch_free(&S, rc == 0);
   for (int k = 0; k < 2; ++k)
     if (ev[k]) (void) hipEventDestroy(ev[k]);
+  g_stats.setup_seconds += now_s() - tt;
+  scratch_free(&S, rc == 0);
   free(want);
   free(D);
   free(host);
@@ -1472,7 +1506,7 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   redset_hip_transport tr;
   redset_hip_mpi_transport* mt = NULL;
   if (choose_exchange(comm, p, r, 1, &mode, &tr, &mt)) {
-    redset_hip_mpi_transport_destroy(mt);
+    transport_done(mt);
     return REDSET_FAILURE;
   }
   g_last_exchange = mode;
@@ -1481,7 +1515,7 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
                                 header, hrc, chunk_size, slice_bytes(B, chunk_size, (size_t) (4 * p + 2 * missing)))
                : sharded_slot(0, rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
                               header, hrc, chunk_size, B, &tr, mt);
-  redset_hip_mpi_transport_destroy(mt);
+  transport_done(mt);
   return stats_end(t0, rc);
 }
 
@@ -1503,7 +1537,7 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   redset_hip_transport tr;
   redset_hip_mpi_transport* mt = NULL;
   if (choose_exchange(comm, p, r, 1, &mode, &tr, &mt)) {
-    redset_hip_mpi_transport_destroy(mt);
+    transport_done(mt);
     return REDSET_FAILURE;
   }
   g_last_exchange = mode;
@@ -1511,7 +1545,7 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
                ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B)
                : sharded_slot(0, NULL, comm, p, r, 1, 1, &root, r == root, lofi, chunk_file, fd_chunk, header, hrc,
                               chunk_size, B, &tr, mt);
-  redset_hip_mpi_transport_destroy(mt);
+  transport_done(mt);
   return stats_end(t0, rc);
 }
 
@@ -1538,7 +1572,7 @@ static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_
   redset_hip_transport tr;
   redset_hip_mpi_transport* mt = NULL;
   if (choose_exchange(comm, p, r, 0, &mode, &tr, &mt)) {
-    redset_hip_mpi_transport_destroy(mt);
+    transport_done(mt);
     return REDSET_FAILURE;
   }
   g_last_exchange = mode;
@@ -1553,7 +1587,7 @@ static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_
     rc = sharded_slot(1, rs, comm, p, r, e, 0, NULL, 0, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B, &tr,
                       mt);
   }
-  redset_hip_mpi_transport_destroy(mt);
+  transport_done(mt);
   return rc;
 }
 

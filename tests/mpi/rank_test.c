@@ -72,17 +72,18 @@ static const char* exchange_name(int m) {
 /* the last call's accounting (redset_hip_rank_last_stats), max and sum over
  * the ranks, as one JSON line from rank 0 (tools/rank_bench.py reads it) */
 static void print_stats(int rank, const char* tag) {
-  enum { NS = 15 };
+  enum { NS = 16 };
   static const char* names[NS] = {"seconds", "read_seconds", "mpi_seconds", "gpu_seconds", "write_seconds",
                                   "read_bytes", "sent_bytes", "recv_bytes", "h2d_bytes", "d2h_bytes", "write_bytes",
-                                  "stage_seconds", "copy_seconds", "plan_seconds", "exchange_seconds"};
+                                  "stage_seconds", "copy_seconds", "plan_seconds", "exchange_seconds",
+                                  "setup_seconds"};
   redset_hip_rank_stats st;
   memset(&st, 0, sizeof(st));
   (void) redset_hip_rank_last_stats(&st);
   double v[NS] = {st.seconds, st.read_seconds, st.mpi_seconds, st.gpu_seconds, st.write_seconds,
                   (double) st.read_bytes, (double) st.sent_bytes, (double) st.recv_bytes, (double) st.h2d_bytes,
                   (double) st.d2h_bytes, (double) st.write_bytes, st.stage_seconds, st.copy_seconds,
-                  st.plan_seconds, st.exchange_seconds};
+                  st.plan_seconds, st.exchange_seconds, st.setup_seconds};
   double mx[NS], sm[NS];
   MPI_Reduce(v, mx, NS, MPI_DOUBLE, MPI_MAX, 0, MPI_COMM_WORLD);
   MPI_Reduce(v, sm, NS, MPI_DOUBLE, MPI_SUM, 0, MPI_COMM_WORLD);

@@ -273,7 +273,7 @@ def test_sharded_slot_round_trip(stub, oracle, tmp_path, scheme, p, e, lost, win
     for res in (enc, reb):
         st = _stats(res.stdout, "warm")
         classes = ["read_seconds", "mpi_seconds", "gpu_seconds", "write_seconds", "stage_seconds", "copy_seconds",
-                   "plan_seconds"]
+                   "plan_seconds", "setup_seconds"]
         # the disjoint classes never exceed the call (per rank: compare sums)
         assert sum(st[k][1] for k in classes) <= st["seconds"][1] * 1.0001, st
         assert st["exchange_seconds"][0] > 0 and st["plan_seconds"][0] > 0, st

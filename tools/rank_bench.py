@@ -25,7 +25,7 @@ MIB = 1 << 20
 
 # the disjoint classes of a call's blocked host time (include/redset_hip_mpi.h)
 BLOCKED = ("read_seconds", "mpi_seconds", "gpu_seconds", "write_seconds", "stage_seconds", "copy_seconds",
-           "plan_seconds")
+           "plan_seconds", "setup_seconds")
 
 
 def roofline(stats, p, mpi_gbps, pcie_gbps, seconds):

@@ -307,7 +307,9 @@ static void scratch_release(scratch* S, int ok) {
   S->nbuf = 0;
 }
 
+static void exch_release_all(void);
 void redset_hip_rank_scratch_release(void) {
+  exch_release_all();
   pthread_mutex_lock(&pool_mu);
   for (int i = 0; i < npool; ++i) release(&pool[i]);
   npool = 0;
@@ -1149,22 +1151,119 @@ int redset_hip_rank_set_exchange(int mode) {
 
 int redset_hip_rank_last_exchange(void) { return g_last_exchange; }
 
-/* per-communicator exchange, decided once and cached on the communicator
- * (an MPI attribute: the RCCL communicator is destroyed with it) */
+/* What the sharded slot keeps from one call to the next on a communicator
+ * (a "slot context"): its pinned window images, device slabs, stream,
+ * events and the sharded plans of every window, for one call shape. A
+ * checkpoint loop calls the same shape again and again, and planning, the
+ * plans' streams, the pinned images and the slabs are then set up once
+ * instead of per call (round 5: they were ~20% of a warm call on one box,
+ * profiles/r05s4_rank_roofline.jsonl). Another shape replaces it; a failed
+ * call frees it; REDSET_HIP_SCRATCH_CACHE=0 or redset_hip_rank_scratch_release
+ * frees it too. */
 typedef struct {
+  /* the shape it serves */
+  int encode, xor_scheme, p, e, missing, lost[256], r, device;
+  size_t chunk_size, win;
+  redset_hip_transport tr;
+  /* what it holds */
+  size_t W, WW, nwin, tail, xbytes, xmsgs;
+  unsigned char* want;
+  uint8_t *h_img[2], *hd[2], *hp[2], *gd[2], *gp[2];
+  redset_hip_sharded* plan[2][2]; /* [buffer][tail window] */
+  hipEvent_t ev[2];
+  hipStream_t stream;
+} slot_ctx;
+
+static void slot_ctx_free(slot_ctx* C) {
+  if (!C) return;
+  if (C->stream) (void) hipStreamSynchronize(C->stream);
+  for (int b = 0; b < 2; ++b) {
+    for (int t = 0; t < 2; ++t) redset_hip_sharded_destroy(C->plan[b][t]);
+    if (C->ev[b]) (void) hipEventDestroy(C->ev[b]);
+    if (C->h_img[b]) (void) hipHostFree(C->h_img[b]);
+    uint8_t* dev[4] = {C->hd[b], C->hp[b], C->gd[b], C->gp[b]};
+    for (int k = 0; k < 4; ++k)
+      if (dev[k]) (void) hipFree(dev[k]);
+  }
+  if (C->stream) (void) hipStreamDestroy(C->stream);
+  free(C->want);
+  free(C);
+}
+
+/* per-communicator exchange, decided once and cached on the communicator
+ * (an MPI attribute: the RCCL communicator, a _SHARDED_MPI transport and the
+ * slot context are destroyed with it) */
+typedef struct {
+  int decided;             /* the RCCL decision has been made */
   int mode;                /* REDSET_HIP_EXCHANGE_HOST_MPI or _SHARDED_RCCL */
   redset_hip_transport tr;
   redset_hip_rccl* rccl;
+  redset_hip_transport mt_tr;  /* _SHARDED_MPI: the MPI transport with device buffers */
+  redset_hip_mpi_transport* mt;
+  slot_ctx* ctx;
 } comm_exchange;
+
+/* every live comm_exchange, so redset_hip_rank_scratch_release can free
+ * what they cache */
+#define MAX_EXCH 64
+static pthread_mutex_t exch_mu = PTHREAD_MUTEX_INITIALIZER;
+static comm_exchange* exch_live[MAX_EXCH];
+
+static void exch_register(comm_exchange* X, int add) {
+  pthread_mutex_lock(&exch_mu);
+  for (int i = 0; i < MAX_EXCH; ++i) {
+    if (add && !exch_live[i]) {
+      exch_live[i] = X;
+      break;
+    }
+    if (!add && exch_live[i] == X) exch_live[i] = NULL;
+  }
+  pthread_mutex_unlock(&exch_mu);
+}
+
+/* the communicator's cached sharded resources, freed (the RCCL communicator stays) */
+static void exch_release(comm_exchange* X) {
+  slot_ctx_free(X->ctx);
+  X->ctx = NULL;
+  redset_hip_mpi_transport_destroy(X->mt);
+  X->mt = NULL;
+}
 
 static int exch_keyval = MPI_KEYVAL_INVALID;
 
 static int exch_delete(MPI_Comm comm, int keyval, void* attr, void* extra) {
   (void) comm, (void) keyval, (void) extra;
   comm_exchange* X = (comm_exchange*) attr;
-  if (X) redset_hip_rccl_transport_destroy(X->rccl);
+  if (X) {
+    exch_register(X, 0);
+    exch_release(X);
+    redset_hip_rccl_transport_destroy(X->rccl);
+  }
   free(X);
   return MPI_SUCCESS;
+}
+
+/* the communicator's comm_exchange, made on first use (local) */
+static int exch_get(MPI_Comm comm, comm_exchange** out) {
+  *out = NULL;
+  if (exch_keyval == MPI_KEYVAL_INVALID &&
+      MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, exch_delete, &exch_keyval, NULL) != MPI_SUCCESS)
+    return fail("MPI_Comm_create_keyval failed");
+  comm_exchange* X = NULL;
+  int found = 0;
+  if (MPI_Comm_get_attr(comm, exch_keyval, &X, &found) != MPI_SUCCESS) return fail("MPI_Comm_get_attr failed");
+  if (!found) {
+    X = calloc(1, sizeof(*X));
+    if (!X) return fail("out of host memory");
+    X->mode = REDSET_HIP_EXCHANGE_HOST_MPI;
+    if (MPI_Comm_set_attr(comm, exch_keyval, X) != MPI_SUCCESS) {
+      free(X);
+      return fail("MPI_Comm_set_attr failed");
+    }
+    exch_register(X, 1);
+  }
+  *out = X;
+  return 0;
 }
 
 /* members on one node, each with its own GPU, and librccl loadable on every
@@ -1224,65 +1323,55 @@ static int rccl_create(MPI_Comm comm, int p, int r, comm_exchange* X) {
  * host path. AUTO keeps the encodes on the host path: north_star asks for
  * RCCL "only for the multi-rank rebuild case", and an encode over RCCL has
  * not yet run on a node with a GPU per member; forcing
- * _SHARDED_RCCL still sends an encode there. *tr is set for the sharded
- * modes; *mpi_t is a transport to destroy after the call (SHARDED_MPI). */
-static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, redset_hip_transport* tr,
-                               redset_hip_mpi_transport** mpi_t);
-static int choose_exchange(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, redset_hip_transport* tr,
-                           redset_hip_mpi_transport** mpi_t) {
+ * _SHARDED_RCCL still sends an encode there. For the sharded modes *xo is
+ * the communicator's comm_exchange: its transport (RCCL, or the _SHARDED_MPI
+ * transport, made on first use and kept) and its slot context. */
+static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, comm_exchange** xo);
+static int choose_exchange(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, comm_exchange** xo) {
   const double t0 = now_s();
-  const int rc = choose_exchange_now(comm, p, r, auto_rccl, mode, tr, mpi_t);
+  const int rc = choose_exchange_now(comm, p, r, auto_rccl, mode, xo);
   g_stats.setup_seconds += now_s() - t0;
   return rc;
 }
-/* the transport of a _SHARDED_MPI call, destroyed after it (its pinned staging goes too) */
-static void transport_done(redset_hip_mpi_transport* mt) {
-  const double t0 = now_s();
-  redset_hip_mpi_transport_destroy(mt);
-  g_stats.setup_seconds += now_s() - t0;
-}
-static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, redset_hip_transport* tr,
-                               redset_hip_mpi_transport** mpi_t) {
+
+static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, comm_exchange** xo) {
   int m[2] = {g_exchange_mode, -g_exchange_mode}, mm[2];
-  *mpi_t = NULL;
+  *xo = NULL;
   if (MPI_Allreduce(m, mm, 2, MPI_INT, MPI_MAX, comm) != MPI_SUCCESS) return fail("MPI_Allreduce failed");
   if (mm[0] != -mm[1]) return fail("members disagree on the rebuild exchange (redset_hip_rank_set_exchange)");
   *mode = m[0];
   if (*mode == REDSET_HIP_EXCHANGE_AUTO && !auto_rccl) *mode = REDSET_HIP_EXCHANGE_HOST_MPI;
   if (*mode == REDSET_HIP_EXCHANGE_HOST_MPI) return 0;
+  comm_exchange* X = NULL;
+  int rc = exch_get(comm, &X);
   if (*mode == REDSET_HIP_EXCHANGE_SHARDED_MPI) {
     /* the sharded plan over MPI with device buffers staged through pinned
      * memory: members may share a GPU (tests, or nodes without RCCL) */
-    int rc = redset_hip_mpi_transport_create(comm, 1, tr, mpi_t);
-    return agree_setup(comm, rc);
+    if (!rc && !X->mt) rc = redset_hip_mpi_transport_create(comm, 1, &X->mt_tr, &X->mt);
+    if ((rc = agree_setup(comm, rc))) return rc;
+    *xo = X;
+    return 0;
   }
-  if (exch_keyval == MPI_KEYVAL_INVALID &&
-      MPI_Comm_create_keyval(MPI_COMM_NULL_COPY_FN, exch_delete, &exch_keyval, NULL) != MPI_SUCCESS)
-    return fail("MPI_Comm_create_keyval failed");
-  comm_exchange* X = NULL;
-  int found = 0;
-  if (MPI_Comm_get_attr(comm, exch_keyval, &X, &found) != MPI_SUCCESS) return fail("MPI_Comm_get_attr failed");
-  if (!found) {
-    X = calloc(1, sizeof(*X));
-    if (!X) return fail("out of host memory");
-    X->mode = REDSET_HIP_EXCHANGE_HOST_MPI;
+  if ((rc = agree_setup(comm, rc))) return rc;
+  if (!X->decided) {
     if (*mode == REDSET_HIP_EXCHANGE_SHARDED_RCCL || rccl_possible(comm, p, r)) {
       if (rccl_create(comm, p, r, X) == 0) X->mode = REDSET_HIP_EXCHANGE_SHARDED_RCCL;
-      else if (*mode == REDSET_HIP_EXCHANGE_SHARDED_RCCL) {
-        free(X);
-        return REDSET_FAILURE;
-      }
+      else if (*mode == REDSET_HIP_EXCHANGE_SHARDED_RCCL) return REDSET_FAILURE;
     }
-    if (MPI_Comm_set_attr(comm, exch_keyval, X) != MPI_SUCCESS) {
-      exch_delete(comm, exch_keyval, X, NULL);
-      return fail("MPI_Comm_set_attr failed");
-    }
+    X->decided = 1;
   }
   if (*mode == REDSET_HIP_EXCHANGE_SHARDED_RCCL && X->mode != REDSET_HIP_EXCHANGE_SHARDED_RCCL)
     return fail("RCCL exchange requested, but this communicator uses the host path");
   *mode = X->mode;
-  *tr = X->tr;
+  *xo = X;
   return 0;
+}
+
+static void exch_release_all(void) {
+  pthread_mutex_lock(&exch_mu);
+  for (int i = 0; i < MAX_EXCH; ++i)
+    if (exch_live[i]) exch_release(exch_live[i]);
+  pthread_mutex_unlock(&exch_mu);
 }
 
 /* member r's cell in stripe c: data cell x (0 <= x < d) or parity slot
@@ -1293,15 +1382,123 @@ static int member_cell(int p, int e, int xor_scheme, int r, int c) {
   return enc < p ? redset_hip_rs_get_data_id(p, e, r, c) : (p - e) + (enc - p);
 }
 
+/* The slot context for this call: the communicator's cached one when it
+ * serves this shape, else a new one -- buffers, stream, events, the cells of
+ * mine the exchange reads, and the plans of every window (planning is
+ * local: no communication, every member the same), with the MPI transport's
+ * staging and requests sized for the largest exchange, so no exchange
+ * allocates (a failed allocation there would leave the peers waiting).
+ * Returns the context, or NULL with *rc set. */
+static slot_ctx* slot_ctx_get(comm_exchange* X, const redset_hip_transport* tr, redset_hip_mpi_transport* mt,
+                              int encode, const redset_hip_rs* rs, int p, int r, int e, int missing, const int* lost,
+                              int need_rebuild, size_t chunk_size, size_t win, int* rc) {
+  const int xor_scheme = rs == NULL, d = p - e, ncell = p, world = p;
+  int device = -1;
+  (void) hipGetDevice(&device);
+  slot_ctx* C = X->ctx;
+  if (C) {
+    int same = C->encode == encode && C->xor_scheme == xor_scheme && C->p == p && C->e == e &&
+               C->missing == missing && C->r == r && C->device == device && C->chunk_size == chunk_size &&
+               C->win == win && C->tr.exchange == tr->exchange && C->tr.ctx == tr->ctx;
+    for (int i = 0; i < missing && same; ++i) same = C->lost[i] == lost[i];
+    if (same) return C;
+    X->ctx = NULL;
+    slot_ctx_free(C);
+  }
+  C = calloc(1, sizeof(*C));
+  if (!C) {
+    *rc = fail("out of host memory");
+    return NULL;
+  }
+  C->encode = encode, C->xor_scheme = xor_scheme, C->p = p, C->e = e, C->missing = missing, C->r = r;
+  C->device = device, C->chunk_size = chunk_size, C->win = win, C->tr = *tr;
+  for (int i = 0; i < missing; ++i) C->lost[i] = lost[i];
+  C->W = redset_hip_shard_slice_bytes(win, world);
+  C->WW = C->W * (size_t) world; /* one cell's window in the host image */
+  C->nwin = chunk_size ? (chunk_size + win - 1) / win : 0;
+  C->tail = chunk_size - (C->nwin ? (C->nwin - 1) * win : 0);
+  const double t0 = now_s();
+  int err = 0;
+  const size_t W = C->W;
+  for (int b = 0; b < 2 && !err; ++b) {
+    if (hipHostMalloc((void**) &C->h_img[b], (size_t) ncell * C->WW, hipHostMallocDefault) != hipSuccess ||
+        hipMalloc((void**) &C->hd[b], (size_t) world * d * W) != hipSuccess ||
+        hipMalloc((void**) &C->hp[b], (size_t) world * e * W) != hipSuccess ||
+        hipMalloc((void**) &C->gd[b], (size_t) world * d * W) != hipSuccess ||
+        hipMalloc((void**) &C->gp[b], (size_t) world * e * W) != hipSuccess)
+      err = fail("sharded slot: allocating %zu B of window buffers failed", (size_t) ncell * C->WW);
+    if (!err && hipEventCreateWithFlags(&C->ev[b], hipEventDisableTiming) != hipSuccess) err = fail("hipEventCreate failed");
+  }
+  if (!err && hipStreamCreateWithFlags(&C->stream, hipStreamNonBlocking) != hipSuccess) {
+    C->stream = NULL;
+    err = fail("hipStreamCreate failed");
+  }
+  C->want = calloc((size_t) ncell, 1); /* cells of mine some stripe's decode reads */
+  unsigned char* D = malloc((size_t) (missing > 0 ? missing : 1) * p);
+  int* host = malloc(sizeof(int) * (size_t) p);
+  int* slot = calloc((size_t) p, sizeof(int));
+  if (!err && (!C->want || !D || !host || !slot)) err = fail("out of host memory");
+  g_stats.setup_seconds += now_s() - t0;
+  /* which of my cells the exchange reads: the encode every data cell, the
+   * decode those its maps read (the sharded plan sends exactly those) */
+  for (int x = 0; x < d && encode && !err; ++x) C->want[x] = 1;
+  for (int c = 0; c < p && !err && !need_rebuild && !encode; ++c) {
+    int used = xor_scheme;
+    if (!xor_scheme) {
+      err = redset_hip_rs_decode_matrix(rs, missing, lost, c, D);
+      for (int i = 0; i < missing && !err; ++i) used |= D[(size_t) i * p + r] != 0;
+    }
+    if (used) C->want[member_cell(p, e, xor_scheme, r, c)] = 1;
+  }
+  for (int m = 0; m < p && host; ++m) host[m] = m;
+  /* the plans of buffers b = n & 1 of window n, whole or tail */
+  const double tp = now_s();
+  for (size_t n = 0; n < C->nwin && !err; ++n) {
+    const size_t len = n + 1 == C->nwin ? C->tail : win;
+    const int b = (int) (n & 1);
+    redset_hip_sharded** P = &C->plan[b][len != win];
+    if (*P) continue;
+    redset_hip_shard_layout L = {1, host, slot, 1, len, W, C->hd[b], C->hp[b], C->gd[b], C->gp[b]};
+    if (encode)
+      err = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, tr, NULL, P)
+                       : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, tr, NULL, P);
+    else
+      err = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, tr, NULL, P)
+                       : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, tr, NULL, P);
+    redset_hip_sharded_info info;
+    if (!err && !(err = redset_hip_sharded_get_info(*P, &info))) {
+      const size_t gb = info.gather_bytes_sent + info.gather_bytes_recv;
+      const size_t rb = info.return_bytes_sent + info.return_bytes_recv;
+      const size_t gm = (size_t) info.gather_messages + (size_t) info.gather_recv_messages;
+      const size_t rm = (size_t) info.return_messages + (size_t) info.return_recv_messages;
+      C->xbytes = gb > C->xbytes ? gb : C->xbytes;
+      C->xbytes = rb > C->xbytes ? rb : C->xbytes;
+      C->xmsgs = gm > C->xmsgs ? gm : C->xmsgs;
+      C->xmsgs = rm > C->xmsgs ? rm : C->xmsgs;
+    }
+  }
+  if (!err && mt) err = redset_hip_mpi_transport_reserve(mt, C->xbytes, C->xmsgs);
+  g_stats.plan_seconds += now_s() - tp;
+  free(D);
+  free(host);
+  free(slot);
+  if (err) {
+    slot_ctx_free(C);
+    *rc = err;
+    return NULL;
+  }
+  return C;
+}
+
 /* The encode (encode = 1: every member's data cells in, its parity cells
- * out) or the rebuild (the lost members' cells) as the sharded plan over a
- * transport. rs == NULL: XOR (e = 1; rebuild: the root is lost[0]). */
+ * out) or the rebuild (the lost members' cells) as the sharded plan over the
+ * communicator's transport (X: RCCL, or the _SHARDED_MPI transport).
+ * rs == NULL: XOR (e = 1; rebuild: the root is lost[0]). */
 static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int p, int r, int e, int missing,
                         const int* lost, int need_rebuild, const redset_hip_io* lofi, const char* chunk_file,
-                        int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B,
-                        const redset_hip_transport* tr, redset_hip_mpi_transport* mt) {
+                        int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B, comm_exchange* X,
+                        int mode) {
   const int d = p - e, ncell = p, world = p;
-  const int xor_scheme = rs == NULL;
   size_t win = SHARDED_WINDOW / (size_t) ncell;
 #if REDSET_HIP_TEST_KNOBS
   /* test builds: small windows, so small sets take several (the mid-call stop) */
@@ -1310,90 +1507,28 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
   if (win < B) win = B;
   if (win > chunk_size) win = chunk_size;
   if (win == 0) win = 1;
-  const size_t W = redset_hip_shard_slice_bytes(win, world);
-  const size_t WW = W * (size_t) world; /* one cell's window in the host image */
-  const size_t nwin = chunk_size ? (chunk_size + win - 1) / win : 0;
-  const size_t tail = chunk_size - (nwin ? (nwin - 1) * win : 0);
-
-  unsigned char* want = calloc((size_t) ncell, 1); /* cells of mine some stripe's decode reads */
-  unsigned char* D = malloc((size_t) (missing > 0 ? missing : 1) * p);
-  int* host = malloc(sizeof(int) * (size_t) p);
-  int* slot = calloc((size_t) p, sizeof(int));
-  scratch S;
-  scratch_init(&S);
-  uint8_t* h_img[2] = {scratch_host(&S, (size_t) ncell * WW), scratch_host(&S, (size_t) ncell * WW)};
-  uint8_t* hd[2] = {scratch_dev(&S, (size_t) world * d * W), scratch_dev(&S, (size_t) world * d * W)};
-  uint8_t* hp[2] = {scratch_dev(&S, (size_t) world * e * W), scratch_dev(&S, (size_t) world * e * W)};
-  uint8_t* gd[2] = {scratch_dev(&S, (size_t) world * d * W), scratch_dev(&S, (size_t) world * d * W)};
-  uint8_t* gp[2] = {scratch_dev(&S, (size_t) world * e * W), scratch_dev(&S, (size_t) world * e * W)};
-  redset_hip_sharded* plan[2][2] = {{NULL, NULL}, {NULL, NULL}}; /* [buffer][tail window] */
-  hipEvent_t ev[2] = {NULL, NULL};
-  int rc = S.rc ? S.rc : hrc;
-  const double te = now_s();
-  for (int k = 0; k < 2 && !rc; ++k)
-    if (hipEventCreateWithFlags(&ev[k], hipEventDisableTiming) != hipSuccess) rc = fail("hipEventCreate failed");
-  g_stats.setup_seconds += now_s() - te;
-  if (!rc && (!want || !D || !host || !slot)) rc = fail("out of host memory");
+  int rc = hrc;
   if (!rc && need_rebuild && !lofi->write) rc = fail("lofi has no write callback");
-  /* which of my cells the exchange reads: the encode every data cell, the
-   * decode those its maps read (the sharded plan sends exactly those) */
-  for (int x = 0; x < d && encode && want; ++x) want[x] = 1;
-  for (int c = 0; c < p && !rc && !need_rebuild && !encode; ++c) {
-    int used = xor_scheme;
-    if (!xor_scheme) {
-      rc = redset_hip_rs_decode_matrix(rs, missing, lost, c, D);
-      for (int i = 0; i < missing && !rc; ++i) used |= D[(size_t) i * p + r] != 0;
-    }
-    if (used) want[member_cell(p, e, xor_scheme, r, c)] = 1;
-  }
-  for (int m = 0; m < p && host; ++m) host[m] = m;
-  /* the plans of every window before the agreement (planning is local: no
-   * communication, every member the same): buffers b = n & 1 of window n,
-   * for a whole window or the tail one. Over the MPI transport, its staging
-   * and requests are sized here for the largest exchange, so no exchange
-   * allocates (a failed allocation there would leave the peers waiting) */
-  const double tp = now_s();
-  size_t xbytes = 0, xmsgs = 0;
-  for (size_t n = 0; n < nwin && !rc; ++n) {
-    const size_t len = n + 1 == nwin ? tail : win;
-    const int b = (int) (n & 1);
-    redset_hip_sharded** P = &plan[b][len != win];
-    if (*P) continue;
-    redset_hip_shard_layout L = {1, host, slot, 1, len, W, hd[b], hp[b], gd[b], gp[b]};
-    if (encode)
-      rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, tr, NULL, P)
-                      : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, tr, NULL, P);
-    else
-      rc = xor_scheme ? redset_hip_xor_sharded_plan(p, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, tr, NULL, P)
-                      : redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, tr, NULL, P);
-    redset_hip_sharded_info info;
-    if (!rc && !(rc = redset_hip_sharded_get_info(*P, &info))) {
-      const size_t gb = info.gather_bytes_sent + info.gather_bytes_recv;
-      const size_t rb = info.return_bytes_sent + info.return_bytes_recv;
-      const size_t gm = (size_t) info.gather_messages + (size_t) info.gather_recv_messages;
-      const size_t rm = (size_t) info.return_messages + (size_t) info.return_recv_messages;
-      xbytes = gb > xbytes ? gb : xbytes;
-      xbytes = rb > xbytes ? rb : xbytes;
-      xmsgs = gm > xmsgs ? gm : xmsgs;
-      xmsgs = rm > xmsgs ? rm : xmsgs;
-    }
-  }
-  if (!rc && mt) rc = redset_hip_mpi_transport_reserve(mt, xbytes, xmsgs);
-  g_stats.plan_seconds += now_s() - tp;
+  int crc = 0;
+  /* the mode's transport: RCCL, or the MPI transport with device buffers */
+  const int over_mpi = mode == REDSET_HIP_EXCHANGE_SHARDED_MPI;
+  slot_ctx* C = slot_ctx_get(X, over_mpi ? &X->mt_tr : &X->tr, over_mpi ? X->mt : NULL, encode, rs, p, r, e, missing,
+                             lost, need_rebuild, chunk_size, win, &crc);
+  if (!rc) rc = crc;
   if ((rc = agree_setup(comm, rc))) goto out;
 
-  int stopped = 0;
+  const size_t W = C->W, WW = C->WW, nwin = C->nwin, tail = C->tail;
   for (size_t n = 0; n <= nwin; ++n) {
     const int b = (int) (n & 1);
     const size_t off = n * win, len = n + 1 == nwin ? tail : win;
     if (n < nwin) {
       /* buffers b were last used by window n - 2, written at window n - 1 */
-      if (n >= 2 && !rc && ev_wait(ev[b])) rc = REDSET_FAILURE;
+      if (n >= 2 && !rc && ev_wait(C->ev[b])) rc = REDSET_FAILURE;
       /* the plan of buffers b for a whole window, or for the tail window */
-      redset_hip_sharded** P = &plan[b][len != win];
-      uint8_t* img = h_img[b];
+      redset_hip_sharded* P = C->plan[b][len != win];
+      uint8_t* img = C->h_img[b];
       for (int x = 0; x < ncell && !rc; ++x) {
-        if (!want[x]) continue;
+        if (!C->want[x]) continue;
         uint8_t* dst = img + (size_t) x * WW;
         if (x < d) {
           if (io_read(lofi, x, off, len, dst) != 0) rc = fail("lofi read failed");
@@ -1408,15 +1543,14 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
       g_stats.mpi_seconds += now_s() - ta;
       if (!all) {
         if (!rc) rc = fail("a peer's read or device step failed");
-        stopped = 1;
         break;
       }
-      hipStream_t s = S.stream;
+      hipStream_t s = C->stream;
       if (!rc) rc = injected_device_failure(comm);
       double tc = now_s();
       for (int x = 0; x < ncell && !rc; ++x) {
-        if (!want[x]) continue;
-        uint8_t* dst = x < d ? hd[b] + (size_t) x * W : hp[b] + (size_t) (x - d) * W;
+        if (!C->want[x]) continue;
+        uint8_t* dst = x < d ? C->hd[b] + (size_t) x * W : C->hp[b] + (size_t) (x - d) * W;
         const size_t dpitch = (size_t) (x < d ? d : e) * W;
         if (hipMemcpy2DAsync(dst, dpitch, img + (size_t) x * WW, W, W, (size_t) world, hipMemcpyHostToDevice, s) !=
             hipSuccess)
@@ -1428,20 +1562,20 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
        * its peers are in it (a member whose copies failed sends what its
        * buffers hold, and every member stops at the next window's agreement) */
       const double tx = now_s();
-      if (!*P) {
+      if (!P) {
         if (!rc) rc = fail("sharded window without a plan");
-      } else if (redset_hip_sharded_execute(*P, s) != 0 && !rc) {
+      } else if (redset_hip_sharded_execute(P, s) != 0 && !rc) {
         rc = REDSET_FAILURE;
       }
       g_stats.exchange_seconds += now_s() - tx;
       redset_hip_sharded_info info;
-      if (!rc && redset_hip_sharded_get_info(*P, &info) == 0) {
+      if (!rc && redset_hip_sharded_get_info(P, &info) == 0) {
         g_stats.sent_bytes += info.gather_bytes_sent + info.return_bytes_sent;
         g_stats.recv_bytes += info.gather_bytes_recv + info.return_bytes_recv;
       }
       tc = now_s();
       for (int x = encode ? d : 0; x < ncell && !rc && (need_rebuild || encode); ++x) {
-        const uint8_t* src = x < d ? hd[b] + (size_t) x * W : hp[b] + (size_t) (x - d) * W;
+        const uint8_t* src = x < d ? C->hd[b] + (size_t) x * W : C->hp[b] + (size_t) (x - d) * W;
         const size_t spitch = (size_t) (x < d ? d : e) * W;
         if (hipMemcpy2DAsync(img + (size_t) x * WW, W, src, spitch, W, (size_t) world, hipMemcpyDeviceToHost, s) !=
             hipSuccess)
@@ -1449,16 +1583,16 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
         g_stats.d2h_bytes += WW;
       }
       g_stats.copy_seconds += now_s() - tc;
-      if (!rc && hipEventRecord(ev[b], s) != hipSuccess) rc = fail("hipEventRecord failed");
+      if (!rc && hipEventRecord(C->ev[b], s) != hipSuccess) rc = fail("hipEventRecord failed");
     }
     /* window n - 1's rebuilt cells (encode: parity cells), after the header
      * as the host path writes them */
     if (n >= 1 && (need_rebuild || encode) && !rc) {
       const int pb = 1 - b;
       const size_t poff = (n - 1) * win, plen = n == nwin ? tail : win;
-      if (ev_wait(ev[pb])) rc = REDSET_FAILURE;
+      if (ev_wait(C->ev[pb])) rc = REDSET_FAILURE;
       for (int x = encode ? d : 0; x < ncell && !rc; ++x) {
-        const uint8_t* cell = h_img[pb] + (size_t) x * WW;
+        const uint8_t* cell = C->h_img[pb] + (size_t) x * WW;
         if (x < d) {
           if (io_write(lofi, x, poff, plen, cell) != 0) rc = fail("lofi write failed");
         } else if (pwrite_full(fd_chunk, cell, plen, header + (off_t) (x - d) * (off_t) chunk_size + (off_t) poff) != 0) {
@@ -1467,20 +1601,17 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
       }
     }
   }
-  (void) stopped;
 out:;
+  /* the context serves the next call of this shape; a failed call's, or
+   * every call's with the cache off, goes */
   const double tt = now_s();
-  if (S.stream) (void) hipStreamSynchronize(S.stream);
-  for (int b = 0; b < 2; ++b)
-    for (int t = 0; t < 2; ++t) redset_hip_sharded_destroy(plan[b][t]);
-  for (int k = 0; k < 2; ++k)
-    if (ev[k]) (void) hipEventDestroy(ev[k]);
+  if (C && C->stream && hipStreamSynchronize(C->stream) != hipSuccess && !rc) rc = fail("stream sync failed");
+  if (C && (rc || !cache_on())) {
+    slot_ctx_free(C);
+    C = NULL;
+  }
+  X->ctx = C;
   g_stats.setup_seconds += now_s() - tt;
-  scratch_free(&S, rc == 0);
-  free(want);
-  free(D);
-  free(host);
-  free(slot);
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
 }
 
@@ -1503,19 +1634,14 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
   if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
   int mode;
-  redset_hip_transport tr;
-  redset_hip_mpi_transport* mt = NULL;
-  if (choose_exchange(comm, p, r, 1, &mode, &tr, &mt)) {
-    transport_done(mt);
-    return REDSET_FAILURE;
-  }
+  comm_exchange* X = NULL;
+  if (choose_exchange(comm, p, r, 1, &mode, &X)) return REDSET_FAILURE;
   g_last_exchange = mode;
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
                ? rs_decode_host(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
                                 header, hrc, chunk_size, slice_bytes(B, chunk_size, (size_t) (4 * p + 2 * missing)))
                : sharded_slot(0, rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
-                              header, hrc, chunk_size, B, &tr, mt);
-  transport_done(mt);
+                              header, hrc, chunk_size, B, X, mode);
   return stats_end(t0, rc);
 }
 
@@ -1534,18 +1660,13 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
   if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
   int mode;
-  redset_hip_transport tr;
-  redset_hip_mpi_transport* mt = NULL;
-  if (choose_exchange(comm, p, r, 1, &mode, &tr, &mt)) {
-    transport_done(mt);
-    return REDSET_FAILURE;
-  }
+  comm_exchange* X = NULL;
+  if (choose_exchange(comm, p, r, 1, &mode, &X)) return REDSET_FAILURE;
   g_last_exchange = mode;
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
                ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B)
                : sharded_slot(0, NULL, comm, p, r, 1, 1, &root, r == root, lofi, chunk_file, fd_chunk, header, hrc,
-                              chunk_size, B, &tr, mt);
-  transport_done(mt);
+                              chunk_size, B, X, mode);
   return stats_end(t0, rc);
 }
 
@@ -1569,12 +1690,8 @@ static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_
   const size_t B = buf_size ? buf_size : DEFAULT_BUF;
   if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
   int mode;
-  redset_hip_transport tr;
-  redset_hip_mpi_transport* mt = NULL;
-  if (choose_exchange(comm, p, r, 0, &mode, &tr, &mt)) {
-    transport_done(mt);
-    return REDSET_FAILURE;
-  }
+  comm_exchange* X = NULL;
+  if (choose_exchange(comm, p, r, 0, &mode, &X)) return REDSET_FAILURE;
   g_last_exchange = mode;
   int rc;
   if (mode == REDSET_HIP_EXCHANGE_HOST_MPI) {
@@ -1584,10 +1701,9 @@ static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_
     /* a bad fd on one member is agreed on inside, not returned early */
     off_t header;
     const int hrc = header_size(fd_chunk, chunk_file, &header);
-    rc = sharded_slot(1, rs, comm, p, r, e, 0, NULL, 0, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B, &tr,
-                      mt);
+    rc = sharded_slot(1, rs, comm, p, r, e, 0, NULL, 0, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B, X,
+                      mode);
   }
-  transport_done(mt);
   return rc;
 }
 

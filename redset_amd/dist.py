@@ -179,6 +179,12 @@ class ShardedSetRunner:
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         L = _lib.load()
         self.W = int(L.redset_hip_shard_slice_bytes(chunk, world))
+        if world == 1:
+            # one process: no slice crosses a link, so the slab pitch can carry
+            # the library's cell pad (redset_hip_cell_stride: 64 MiB cells
+            # otherwise start at equal addresses modulo 2^26 and crowd the
+            # same DRAM channels, the whole-set plans' 2% lesson)
+            self.W = int(L.redset_hip_cell_stride(chunk))
         self.my_len = self.slice_len(rank)
         self._place()
         self.timing = self.device.type == "cuda"

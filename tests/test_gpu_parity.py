@@ -568,9 +568,9 @@ def test_full_size_xor_c2(rd, oracle):
 
 def test_sharded_runner_world1_hip(rd, oracle):
     """redset_amd.dist at world size 1: the C sharded plan (column-slab
-    layout, HIP plans over gathered slices) with the RCCL transport (a
-    one-rank communicator; the exchanges are local copies), checked against
-    the oracle."""
+    layout, the process's own slices computed in place, the slab pitch padded
+    past the chunk) with the RCCL transport (a one-rank communicator with
+    nothing to send), checked against the oracle."""
     from redset_amd.dist import ShardedSetRunner
 
     p, e, chunk = 11, 3, 300_000

@@ -120,12 +120,17 @@ int redset_hip_rank_last_stats(redset_hip_rank_stats* out);
  * paths a few buffers of buf_size; the sharded exchanges two window images
  * of 96 MiB, plus, over the MPI transport (_SHARDED_MPI), a staging buffer of
  * one exchange's bytes sent and received (up to ~2 x 96 MiB).
- * The backends keep a successful call's pinned host buffers, device buffers
- * and stream for the next call (at most 256 MiB pinned, 1 GiB of device
- * memory); REDSET_HIP_SCRATCH_CACHE=0 allocates and frees per call instead,
- * as the reference does (src/redset_reedsolomon.c:298-302, :397-399). This
- * frees the cache (and redset_hip_release_scratch's), e.g. from
- * redset_finalize. */
+ * The host paths keep a successful call's pinned host buffers, device
+ * buffers and stream for the next call (at most 256 MiB pinned, 1 GiB of
+ * device memory). The sharded exchanges keep, per communicator, the last
+ * call shape's context -- its plans and their streams, the two window images
+ * (192 MiB pinned), the device slabs (about 4 x 96 MiB) and, for
+ * _SHARDED_MPI, the transport with its staging -- so a checkpoint loop plans
+ * and allocates once; another shape replaces it, a failed call frees it, and
+ * freeing the communicator frees it. REDSET_HIP_SCRATCH_CACHE=0 allocates
+ * and frees all of it per call instead, as the reference does
+ * (src/redset_reedsolomon.c:298-302, :397-399). This frees every cache (and
+ * redset_hip_release_scratch's), e.g. from redset_finalize. */
 void redset_hip_rank_scratch_release(void);
 
 /* Transport of the sharded path (redset_hip_rs_sharded_plan) over MPI

@@ -509,6 +509,13 @@ static int execute_pipelined(redset_hip_sharded* P, hipStream_t s) {
   hipError_t e;
   int rc = 0;
   const int n = P->info.nsets;
+  if (P->gather.n == 0 && P->ret.n == 0) {
+    /* nothing to exchange (one process, or only its own slices): the
+     * computes alone, on the caller's stream, with no second stream to
+     * order against */
+    for (int k = 0; k < n && !rc; ++k) rc = compute_set(P, k, s);
+    return rc;
+  }
   if (!P->xstream && !P->ev_c) {
     P->ev_c = calloc((size_t) n, sizeof(hipEvent_t));
     if (!P->ev_c) rc = sfail("out of host memory");

@@ -17,6 +17,13 @@ on a healthy GPU:
   taking a batch from its queue and recording it, the window in which a
   stopping loader once could end the block's sequence without that batch
   (codec_device.h gf_mac_claimed CLAIMER_DONE).
+* REDSET_HIP_TEST_HANG_CAP / _TABLE_DELAY (round 5): the cap of the waits
+  with no fallback and a loader that publishes a job's tables late, so the
+  hang word (include/redset_hip.h redset_hip_hang_faults) can be made to
+  count and the per-rank backends to fail the call
+  (tests/test_gpu_hang_contract.py, test_gpu_mpi.py::test_mpi_hang_cap_*).
+  In the runs below the hang cap stays at the product's 2^26 polls, and every
+  test asserts the hang word is 0.
 * REDSET_HIP_SEQUENTIAL / _STREAM_JOBS / _STRIPES_PER_LAUNCH / _XOR_STREAM /
   _ZERO_COPY (tests marked `knobs`): every job order and pipeline mode at
   small sizes.

@@ -130,7 +130,9 @@ int redset_hip_rank_last_stats(redset_hip_rank_stats* out);
  * freeing the communicator frees it. REDSET_HIP_SCRATCH_CACHE=0 allocates
  * and frees all of it per call instead, as the reference does
  * (src/redset_reedsolomon.c:298-302, :397-399). This frees every cache (and
- * redset_hip_release_scratch's), e.g. from redset_finalize. */
+ * redset_hip_release_scratch's), e.g. from redset_finalize; a communicator
+ * whose sharded call is running in another thread keeps its context and
+ * transport until it is freed. */
 void redset_hip_rank_scratch_release(void);
 
 /* Transport of the sharded path (redset_hip_rs_sharded_plan) over MPI

@@ -1201,6 +1201,7 @@ typedef struct {
   redset_hip_transport mt_tr;  /* _SHARDED_MPI: the MPI transport with device buffers */
   redset_hip_mpi_transport* mt;
   slot_ctx* ctx;
+  int busy;                /* a sharded call is using mt / ctx (under exch_mu) */
 } comm_exchange;
 
 /* every live comm_exchange, so redset_hip_rank_scratch_release can free
@@ -1327,6 +1328,7 @@ static int rccl_create(MPI_Comm comm, int p, int r, comm_exchange* X) {
  * the communicator's comm_exchange: its transport (RCCL, or the _SHARDED_MPI
  * transport, made on first use and kept) and its slot context. */
 static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, comm_exchange** xo);
+static void exch_busy(comm_exchange* X, int busy);
 static int choose_exchange(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, comm_exchange** xo) {
   const double t0 = now_s();
   const int rc = choose_exchange_now(comm, p, r, auto_rccl, mode, xo);
@@ -1347,8 +1349,12 @@ static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* 
   if (*mode == REDSET_HIP_EXCHANGE_SHARDED_MPI) {
     /* the sharded plan over MPI with device buffers staged through pinned
      * memory: members may share a GPU (tests, or nodes without RCCL) */
+    if (!rc) exch_busy(X, 1);
     if (!rc && !X->mt) rc = redset_hip_mpi_transport_create(comm, 1, &X->mt_tr, &X->mt);
-    if ((rc = agree_setup(comm, rc))) return rc;
+    if ((rc = agree_setup(comm, rc))) {
+      if (X) exch_busy(X, 0);
+      return rc;
+    }
     *xo = X;
     return 0;
   }
@@ -1363,14 +1369,23 @@ static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* 
   if (*mode == REDSET_HIP_EXCHANGE_SHARDED_RCCL && X->mode != REDSET_HIP_EXCHANGE_SHARDED_RCCL)
     return fail("RCCL exchange requested, but this communicator uses the host path");
   *mode = X->mode;
+  if (*mode != REDSET_HIP_EXCHANGE_HOST_MPI) exch_busy(X, 1); /* until sharded_slot ends */
   *xo = X;
   return 0;
 }
 
+/* a communicator whose sharded call is running keeps its cache: that call
+ * holds the transport and the context */
 static void exch_release_all(void) {
   pthread_mutex_lock(&exch_mu);
   for (int i = 0; i < MAX_EXCH; ++i)
-    if (exch_live[i]) exch_release(exch_live[i]);
+    if (exch_live[i] && !exch_live[i]->busy) exch_release(exch_live[i]);
+  pthread_mutex_unlock(&exch_mu);
+}
+
+static void exch_busy(comm_exchange* X, int busy) {
+  pthread_mutex_lock(&exch_mu);
+  X->busy = busy;
   pthread_mutex_unlock(&exch_mu);
 }
 
@@ -1611,6 +1626,7 @@ out:;
     C = NULL;
   }
   X->ctx = C;
+  exch_busy(X, 0);
   g_stats.setup_seconds += now_s() - tt;
   return rc ? REDSET_FAILURE : REDSET_SUCCESS;
 }

@@ -62,12 +62,20 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
  * onto every member's GPU, runs gf_mac (or the XOR) on each slice and returns
  * the rebuilt slices to the lost members (replacing the decode ring and
  * gather, src/redset_reedsolomon.c:646-733, and the XOR reduce to the root,
- * src/redset_xor.c:466-524). Encodes, and decodes elsewhere, take the
- * host-MPI paths above (north_star: RCCL only for the multi-rank rebuild).
+ * src/redset_xor.c:466-524); decodes elsewhere take the host-MPI paths
+ * above. An RS ENCODE with e >= 2 runs as the sharded plan over host slabs
+ * (_SHARDED_HOST below: it sends (d + e)(p - 1)/p cells per member where the
+ * reference's ring sends d*e, RS(8+3) 10 against 24); XOR and e = 1 encodes,
+ * where the two send the same, take the host ring. AUTO never sends an
+ * encode over RCCL (north_star: RCCL only for the multi-rank rebuild).
  * _HOST_MPI and _SHARDED_RCCL force a path for every call (the encodes too:
  * the parity slices then return to their holders, replacing the encode
  * rings, :329-377, src/redset_xor.c:251-285); _SHARDED_MPI runs the sharded
- * plan over the MPI transport with device buffers (members may share a GPU).
+ * plan over the MPI transport with device buffers (members may share a GPU);
+ * _SHARDED_HOST runs it over the MPI transport with every slab in page-locked
+ * host memory, read and written in place by the kernels over PCIe (no
+ * staging, no copies; windows on two slab sets, one window's kernels under
+ * the next one's reads and gather).
  * After a local device error a member still takes part in the exchange it
  * is in, so no member waits forever. The RCCL decision is made once per
  * communicator (cached on it as an MPI attribute, with the RCCL
@@ -78,7 +86,8 @@ enum {
   REDSET_HIP_EXCHANGE_AUTO = 0,
   REDSET_HIP_EXCHANGE_HOST_MPI = 1,
   REDSET_HIP_EXCHANGE_SHARDED_MPI = 2,
-  REDSET_HIP_EXCHANGE_SHARDED_RCCL = 3
+  REDSET_HIP_EXCHANGE_SHARDED_RCCL = 3,
+  REDSET_HIP_EXCHANGE_SHARDED_HOST = 4
 };
 int redset_hip_rank_set_exchange(int mode);
 int redset_hip_rank_last_exchange(void);
@@ -119,7 +128,8 @@ int redset_hip_rank_last_stats(redset_hip_rank_stats* out);
  * fit: RS(8+3) at 64 MiB chunks takes 248 MiB to encode); the XOR host
  * paths a few buffers of buf_size; the sharded exchanges two window images
  * of 96 MiB, plus, over the MPI transport (_SHARDED_MPI), a staging buffer of
- * one exchange's bytes sent and received (up to ~2 x 96 MiB).
+ * one exchange's bytes sent and received (up to ~2 x 96 MiB); over host slabs
+ * (_SHARDED_HOST) two slab sets of ~96 MiB and no device memory.
  * The host paths keep a successful call's pinned host buffers, device
  * buffers and stream for the next call (at most 256 MiB pinned, 1 GiB of
  * device memory). The sharded exchanges keep, per communicator, the last

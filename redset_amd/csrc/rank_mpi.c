@@ -1143,7 +1143,7 @@ static int g_exchange_mode = REDSET_HIP_EXCHANGE_AUTO;
 static __thread int g_last_exchange = 0;
 
 int redset_hip_rank_set_exchange(int mode) {
-  if (mode < REDSET_HIP_EXCHANGE_AUTO || mode > REDSET_HIP_EXCHANGE_SHARDED_RCCL)
+  if (mode < REDSET_HIP_EXCHANGE_AUTO || mode > REDSET_HIP_EXCHANGE_SHARDED_HOST)
     return fail("rank_set_exchange: unknown mode %d", mode);
   g_exchange_mode = mode;
   return REDSET_SUCCESS;
@@ -1162,16 +1162,20 @@ int redset_hip_rank_last_exchange(void) { return g_last_exchange; }
  * frees it too. */
 typedef struct {
   /* the shape it serves */
-  int encode, xor_scheme, p, e, missing, lost[256], r, device;
+  int host, encode, xor_scheme, p, e, missing, lost[256], r, device;
   size_t chunk_size, win;
   redset_hip_transport tr;
   /* what it holds */
   size_t W, WW, nwin, tail, xbytes, xmsgs;
   unsigned char* want;
+  /* device slabs, double-buffered over the windows, behind pinned window
+   * images; host = 1 (_SHARDED_HOST): one set of slabs in pinned host
+   * memory, no images */
   uint8_t *h_img[2], *hd[2], *hp[2], *gd[2], *gp[2];
   redset_hip_sharded* plan[2][2]; /* [buffer][tail window] */
   hipEvent_t ev[2];
   hipStream_t stream;
+  hipStream_t xs; /* host slabs: the gathers' (idle) stream, so a gather never waits for a compute */
 } slot_ctx;
 
 static void slot_ctx_free(slot_ctx* C) {
@@ -1181,11 +1185,12 @@ static void slot_ctx_free(slot_ctx* C) {
     for (int t = 0; t < 2; ++t) redset_hip_sharded_destroy(C->plan[b][t]);
     if (C->ev[b]) (void) hipEventDestroy(C->ev[b]);
     if (C->h_img[b]) (void) hipHostFree(C->h_img[b]);
-    uint8_t* dev[4] = {C->hd[b], C->hp[b], C->gd[b], C->gp[b]};
+    uint8_t* slab[4] = {C->hd[b], C->hp[b], C->gd[b], C->gp[b]};
     for (int k = 0; k < 4; ++k)
-      if (dev[k]) (void) hipFree(dev[k]);
+      if (slab[k]) (void) (C->host ? hipHostFree(slab[k]) : hipFree(slab[k]));
   }
   if (C->stream) (void) hipStreamDestroy(C->stream);
+  if (C->xs) (void) hipStreamDestroy(C->xs);
   free(C->want);
   free(C);
 }
@@ -1200,6 +1205,8 @@ typedef struct {
   redset_hip_rccl* rccl;
   redset_hip_transport mt_tr;  /* _SHARDED_MPI: the MPI transport with device buffers */
   redset_hip_mpi_transport* mt;
+  redset_hip_transport ht_tr;  /* _SHARDED_HOST: the MPI transport over host slabs */
+  redset_hip_mpi_transport* ht;
   slot_ctx* ctx;
   int busy;                /* a sharded call is using mt / ctx (under exch_mu) */
 } comm_exchange;
@@ -1228,6 +1235,8 @@ static void exch_release(comm_exchange* X) {
   X->ctx = NULL;
   redset_hip_mpi_transport_destroy(X->mt);
   X->mt = NULL;
+  redset_hip_mpi_transport_destroy(X->ht);
+  X->ht = NULL;
 }
 
 static int exch_keyval = MPI_KEYVAL_INVALID;
@@ -1318,39 +1327,56 @@ static int rccl_create(MPI_Comm comm, int p, int r, comm_exchange* X) {
   return 0;
 }
 
+/* What AUTO means for a call (the same on every member):
+ *   AUTO_DECODE       RCCL when the members each own a GPU of one node, else
+ *                     the host path
+ *   AUTO_ENCODE_SLABS the sharded plan over host slabs (_SHARDED_HOST): an RS
+ *                     encode with e >= 2, where it sends (d + e)(p - 1)/p
+ *                     cells per member against the ring's d*e (RS(8+3): 10
+ *                     against 24) and measured faster on one box too
+ *                     (profiles/r05s10_rank_roofline.jsonl)
+ *   AUTO_ENCODE_HOST  the host ring: XOR and RS with e = 1 encodes, where the
+ *                     two send the same bytes
+ * AUTO never sends an encode over RCCL: north_star asks for RCCL "only for
+ * the multi-rank rebuild case", and an encode over RCCL has not yet run on a
+ * node with a GPU per member; forcing _SHARDED_RCCL still does. */
+enum { AUTO_ENCODE_HOST = 0, AUTO_DECODE = 1, AUTO_ENCODE_SLABS = 2 };
+
 /* The exchange of this call (collective): the process's mode -- every
- * member must set the same one -- and, for AUTO, RCCL when the call is a
- * decode (`auto_rccl`) and the members each own a GPU of one node, else the
- * host path. AUTO keeps the encodes on the host path: north_star asks for
- * RCCL "only for the multi-rank rebuild case", and an encode over RCCL has
- * not yet run on a node with a GPU per member; forcing
- * _SHARDED_RCCL still sends an encode there. For the sharded modes *xo is
- * the communicator's comm_exchange: its transport (RCCL, or the _SHARDED_MPI
- * transport, made on first use and kept) and its slot context. */
-static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, comm_exchange** xo);
+ * member must set the same one -- or, for AUTO, what `autop` picks. For the
+ * sharded modes *xo is the communicator's comm_exchange: its transport
+ * (RCCL, or an MPI transport, made on first use and kept) and its slot
+ * context. */
+static int choose_exchange_now(MPI_Comm comm, int p, int r, int autop, int* mode, comm_exchange** xo);
 static void exch_busy(comm_exchange* X, int busy);
-static int choose_exchange(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, comm_exchange** xo) {
+static int choose_exchange(MPI_Comm comm, int p, int r, int autop, int* mode, comm_exchange** xo) {
   const double t0 = now_s();
-  const int rc = choose_exchange_now(comm, p, r, auto_rccl, mode, xo);
+  const int rc = choose_exchange_now(comm, p, r, autop, mode, xo);
   g_stats.setup_seconds += now_s() - t0;
   return rc;
 }
 
-static int choose_exchange_now(MPI_Comm comm, int p, int r, int auto_rccl, int* mode, comm_exchange** xo) {
+static int choose_exchange_now(MPI_Comm comm, int p, int r, int autop, int* mode, comm_exchange** xo) {
   int m[2] = {g_exchange_mode, -g_exchange_mode}, mm[2];
   *xo = NULL;
   if (MPI_Allreduce(m, mm, 2, MPI_INT, MPI_MAX, comm) != MPI_SUCCESS) return fail("MPI_Allreduce failed");
   if (mm[0] != -mm[1]) return fail("members disagree on the rebuild exchange (redset_hip_rank_set_exchange)");
   *mode = m[0];
-  if (*mode == REDSET_HIP_EXCHANGE_AUTO && !auto_rccl) *mode = REDSET_HIP_EXCHANGE_HOST_MPI;
+  if (*mode == REDSET_HIP_EXCHANGE_AUTO && autop == AUTO_ENCODE_HOST) *mode = REDSET_HIP_EXCHANGE_HOST_MPI;
+  if (*mode == REDSET_HIP_EXCHANGE_AUTO && autop == AUTO_ENCODE_SLABS) *mode = REDSET_HIP_EXCHANGE_SHARDED_HOST;
   if (*mode == REDSET_HIP_EXCHANGE_HOST_MPI) return 0;
   comm_exchange* X = NULL;
   int rc = exch_get(comm, &X);
-  if (*mode == REDSET_HIP_EXCHANGE_SHARDED_MPI) {
-    /* the sharded plan over MPI with device buffers staged through pinned
-     * memory: members may share a GPU (tests, or nodes without RCCL) */
+  if (*mode == REDSET_HIP_EXCHANGE_SHARDED_MPI || *mode == REDSET_HIP_EXCHANGE_SHARDED_HOST) {
+    /* the sharded plan over MPI: with device buffers staged through pinned
+     * memory (_SHARDED_MPI), or over slabs in pinned host memory that the
+     * kernels read and write in place (_SHARDED_HOST); members may share a
+     * GPU */
     if (!rc) exch_busy(X, 1);
-    if (!rc && !X->mt) rc = redset_hip_mpi_transport_create(comm, 1, &X->mt_tr, &X->mt);
+    if (!rc && *mode == REDSET_HIP_EXCHANGE_SHARDED_MPI && !X->mt)
+      rc = redset_hip_mpi_transport_create(comm, 1, &X->mt_tr, &X->mt);
+    if (!rc && *mode == REDSET_HIP_EXCHANGE_SHARDED_HOST && !X->ht)
+      rc = redset_hip_mpi_transport_create(comm, 2, &X->ht_tr, &X->ht);
     if ((rc = agree_setup(comm, rc))) {
       if (X) exch_busy(X, 0);
       return rc;
@@ -1404,15 +1430,15 @@ static int member_cell(int p, int e, int xor_scheme, int r, int c) {
  * staging and requests sized for the largest exchange, so no exchange
  * allocates (a failed allocation there would leave the peers waiting).
  * Returns the context, or NULL with *rc set. */
-static slot_ctx* slot_ctx_get(comm_exchange* X, const redset_hip_transport* tr, redset_hip_mpi_transport* mt,
-                              int encode, const redset_hip_rs* rs, int p, int r, int e, int missing, const int* lost,
-                              int need_rebuild, size_t chunk_size, size_t win, int* rc) {
+static slot_ctx* slot_ctx_get(comm_exchange* X, int host_slabs, const redset_hip_transport* tr,
+                              redset_hip_mpi_transport* mt, int encode, const redset_hip_rs* rs, int p, int r, int e,
+                              int missing, const int* lost, int need_rebuild, size_t chunk_size, size_t win, int* rc) {
   const int xor_scheme = rs == NULL, d = p - e, ncell = p, world = p;
   int device = -1;
   (void) hipGetDevice(&device);
   slot_ctx* C = X->ctx;
   if (C) {
-    int same = C->encode == encode && C->xor_scheme == xor_scheme && C->p == p && C->e == e &&
+    int same = C->host == host_slabs && C->encode == encode && C->xor_scheme == xor_scheme && C->p == p && C->e == e &&
                C->missing == missing && C->r == r && C->device == device && C->chunk_size == chunk_size &&
                C->win == win && C->tr.exchange == tr->exchange && C->tr.ctx == tr->ctx;
     for (int i = 0; i < missing && same; ++i) same = C->lost[i] == lost[i];
@@ -1425,7 +1451,7 @@ static slot_ctx* slot_ctx_get(comm_exchange* X, const redset_hip_transport* tr, 
     *rc = fail("out of host memory");
     return NULL;
   }
-  C->encode = encode, C->xor_scheme = xor_scheme, C->p = p, C->e = e, C->missing = missing, C->r = r;
+  C->host = host_slabs, C->encode = encode, C->xor_scheme = xor_scheme, C->p = p, C->e = e, C->missing = missing, C->r = r;
   C->device = device, C->chunk_size = chunk_size, C->win = win, C->tr = *tr;
   for (int i = 0; i < missing; ++i) C->lost[i] = lost[i];
   C->W = redset_hip_shard_slice_bytes(win, world);
@@ -1435,7 +1461,21 @@ static slot_ctx* slot_ctx_get(comm_exchange* X, const redset_hip_transport* tr, 
   const double t0 = now_s();
   int err = 0;
   const size_t W = C->W;
-  for (int b = 0; b < 2 && !err; ++b) {
+  for (int b = 0; b < 2 && !err && host_slabs; ++b) {
+    /* slabs in page-locked host memory: MPI sends and receives them
+     * directly, the kernels read and write them over PCIe */
+    if (hipHostMalloc((void**) &C->hd[b], (size_t) world * d * W, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**) &C->hp[b], (size_t) world * e * W, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**) &C->gd[b], (size_t) world * d * W, hipHostMallocDefault) != hipSuccess ||
+        hipHostMalloc((void**) &C->gp[b], (size_t) world * e * W, hipHostMallocDefault) != hipSuccess)
+      err = fail("sharded slot: allocating %zu B of host slabs failed", (size_t) 2 * ncell * C->WW);
+    if (!err && hipEventCreateWithFlags(&C->ev[b], hipEventDisableTiming) != hipSuccess) err = fail("hipEventCreate failed");
+  }
+  if (!err && host_slabs && hipStreamCreateWithFlags(&C->xs, hipStreamNonBlocking) != hipSuccess) {
+    C->xs = NULL;
+    err = fail("hipStreamCreate failed");
+  }
+  for (int b = 0; b < 2 && !err && !host_slabs; ++b) {
     if (hipHostMalloc((void**) &C->h_img[b], (size_t) ncell * C->WW, hipHostMallocDefault) != hipSuccess ||
         hipMalloc((void**) &C->hd[b], (size_t) world * d * W) != hipSuccess ||
         hipMalloc((void**) &C->hp[b], (size_t) world * e * W) != hipSuccess ||
@@ -1505,16 +1545,10 @@ static slot_ctx* slot_ctx_get(comm_exchange* X, const redset_hip_transport* tr, 
   return C;
 }
 
-/* The encode (encode = 1: every member's data cells in, its parity cells
- * out) or the rebuild (the lost members' cells) as the sharded plan over the
- * communicator's transport (X: RCCL, or the _SHARDED_MPI transport).
- * rs == NULL: XOR (e = 1; rebuild: the root is lost[0]). */
-static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int p, int r, int e, int missing,
-                        const int* lost, int need_rebuild, const redset_hip_io* lofi, const char* chunk_file,
-                        int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B, comm_exchange* X,
-                        int mode) {
-  const int d = p - e, ncell = p, world = p;
-  size_t win = SHARDED_WINDOW / (size_t) ncell;
+/* cell bytes per window of the sharded slot: `budget` over the p cells a
+ * member holds, at least one MPI buffer, at most the chunk */
+static size_t slot_window(size_t budget, size_t chunk_size, int ncell, size_t B) {
+  size_t win = budget / (size_t) ncell;
 #if REDSET_HIP_TEST_KNOBS
   /* test builds: small windows, so small sets take several (the mid-call stop) */
   if (getenv("REDSET_HIP_TEST_SHARDED_WINDOW")) win = (size_t) atoll(getenv("REDSET_HIP_TEST_SHARDED_WINDOW"));
@@ -1522,13 +1556,165 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
   if (win < B) win = B;
   if (win > chunk_size) win = chunk_size;
   if (win == 0) win = 1;
+  return win;
+}
+
+/* the context's epilogue of a sharded call: it serves the next call of this
+ * shape; a failed call's, or every call's with the cache off, goes */
+static int slot_done(comm_exchange* X, slot_ctx* C, int rc) {
+  const double tt = now_s();
+  if (C && C->stream && hipStreamSynchronize(C->stream) != hipSuccess && !rc) rc = fail("stream sync failed");
+  if (C && (rc || !cache_on())) {
+    slot_ctx_free(C);
+    C = NULL;
+  }
+  X->ctx = C;
+  exch_busy(X, 0);
+  g_stats.setup_seconds += now_s() - tt;
+  return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+}
+
+/* _SHARDED_HOST: the sharded plan with every slab in page-locked host
+ * memory. A member reads its cells' window slice by slice straight into its
+ * hosted slabs, MPI sends and receives the slabs themselves, and the gf_mac
+ * (or XOR) kernels read the gathered slices and write the results over PCIe
+ * in place (as the zero-copy streaming path does), so nothing is staged or
+ * copied. What crosses the network per member is the plan's column slices,
+ * (d + e)(p - 1)/p cells for the encode, where the reference's ring sends
+ * every data cell to each of the e parity holders, d*e cells
+ * (src/redset_reedsolomon.c:329-363): RS(8+3) 10 cells instead of 24.
+ * Windows alternate between two slab sets (SHARDED_WINDOW / 2 of cells each,
+ * so both fit the window budget) and their phases overlap: window n's
+ * kernels run on the GPU while the host writes window n - 1, reads window
+ * n + 1 and runs its gather; window n's return follows. Every member runs the
+ * same collectives in the same order: agree(n), gather(n), return(n - 1). */
+static int sharded_slot_host(int encode, const redset_hip_rs* rs, MPI_Comm comm, int p, int r, int e, int missing,
+                             const int* lost, int need_rebuild, const redset_hip_io* lofi, const char* chunk_file,
+                             int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B, comm_exchange* X) {
+  const int d = p - e, ncell = p, world = p;
+  const size_t win = slot_window(SHARDED_WINDOW / 2, chunk_size, ncell, B);
+  int rc = hrc;
+  if (!rc && need_rebuild && !lofi->write) rc = fail("lofi has no write callback");
+  int crc = 0;
+  slot_ctx* C = slot_ctx_get(X, 1, &X->ht_tr, X->ht, encode, rs, p, r, e, missing, lost, need_rebuild, chunk_size,
+                             win, &crc);
+  if (!rc) rc = crc;
+  if ((rc = agree_setup(comm, rc))) return slot_done(X, C, rc);
+
+  const size_t W = C->W, nwin = C->nwin, tail = C->tail;
+  hipStream_t s = C->stream; /* the kernels, and the returns, which wait for them */
+  const int writes = need_rebuild || encode;
+  /* slice q of cell x in the hosted slabs b ([world][1][d][W], [world][1][e][W]) */
+#define HOST_SLICE(b, x, q) ((x) < d ? C->hd[b] + ((size_t) (q) * d + (size_t) (x)) * W \
+                                     : C->hp[b] + ((size_t) (q) * e + (size_t) ((x) - d)) * W)
+#define WIN_LEN(n) ((n) + 1 == nwin ? tail : win)
+  for (size_t n = 0; n <= nwin; ++n) {
+    const int b = (int) (n & 1), pb = 1 - b;
+    redset_hip_sharded* P = n < nwin ? C->plan[b][WIN_LEN(n) != win] : NULL;
+    redset_hip_sharded* Pp = n >= 1 ? C->plan[pb][WIN_LEN(n - 1) != win] : NULL;
+    if (n < nwin) {
+      /* window n into slabs b (last used by window n - 2, whose kernels,
+       * return and writes are done) */
+      const size_t off = n * win, len = WIN_LEN(n);
+      for (int x = 0; x < ncell && !rc; ++x) {
+        if (!C->want[x]) continue;
+        for (size_t q = 0; q < (size_t) world && q * W < len && !rc; ++q) {
+          const size_t lo = q * W, k = min_sz(W, len - lo);
+          if (x < d) {
+            if (io_read(lofi, x, off + lo, k, HOST_SLICE(b, x, q)) != 0) rc = fail("lofi read failed");
+          } else if (pread_full(fd_chunk, HOST_SLICE(b, x, q), k,
+                                header + (off_t) (x - d) * (off_t) chunk_size + (off_t) (off + lo)) != 0) {
+            rc = fail("read %s failed", chunk_file);
+          }
+        }
+      }
+      /* every member's state before the window's exchanges: one failure
+       * stops all (window n - 1's return is skipped by every member alike) */
+      int ok = rc == 0, all = 0;
+      const double ta = now_s();
+      if (MPI_Allreduce(&ok, &all, 1, MPI_INT, MPI_LAND, comm) != MPI_SUCCESS) rc = fail("MPI_Allreduce failed");
+      g_stats.mpi_seconds += now_s() - ta;
+      if (!all) {
+        if (!rc) rc = fail("a peer's read or device step failed");
+        break;
+      }
+      if (!rc) rc = injected_device_failure(comm);
+      if (!P && !rc) rc = fail("sharded window without a plan");
+      /* the gather runs whatever this member's state since the agreement
+       * (its peers are in it), on the idle stream: window n - 1's kernels
+       * keep running */
+      const double tx = now_s();
+      if (P && redset_hip_sharded_execute_phase(P, REDSET_HIP_PHASE_GATHER, C->xs) != 0 && !rc) rc = REDSET_FAILURE;
+      g_stats.exchange_seconds += now_s() - tx;
+    }
+    if (Pp) {
+      /* window n - 1's results back to their holders, after its kernels (the
+       * MPI transport waits for `s` before it posts) */
+      const double tx = now_s();
+      if (redset_hip_sharded_execute_phase(Pp, REDSET_HIP_PHASE_RETURN, s) != 0 && !rc) rc = REDSET_FAILURE;
+      g_stats.exchange_seconds += now_s() - tx;
+    }
+    if (P) {
+      /* window n's kernels, queued behind nothing: the host goes on */
+      if (!rc && redset_hip_sharded_execute_phase(P, REDSET_HIP_PHASE_COMPUTE, s) != 0) rc = REDSET_FAILURE;
+      if (!rc && hipEventRecord(C->ev[b], s) != hipSuccess) rc = fail("hipEventRecord failed");
+      redset_hip_sharded_info info;
+      if (redset_hip_sharded_get_info(P, &info) == 0) {
+        g_stats.sent_bytes += info.gather_bytes_sent + info.return_bytes_sent;
+        g_stats.recv_bytes += info.gather_bytes_recv + info.return_bytes_recv;
+        /* the kernels' PCIe traffic: my slice of every stripe's inputs in,
+         * of its outputs out */
+        const unsigned long long out_b = (unsigned long long) p * (unsigned long long) (encode ? e : missing) *
+                                         info.my_slice_len;
+        g_stats.d2h_bytes += out_b;
+        g_stats.h2d_bytes += info.compute_bytes > out_b ? info.compute_bytes - out_b : 0;
+      }
+    }
+    if (Pp && writes && !rc) {
+      /* window n - 1's rebuilt cells (encode: its parity cells), after the
+       * header as the host path writes them; the slices computed in place
+       * (my own) are done with its kernels */
+      const size_t off = (n - 1) * win, len = WIN_LEN(n - 1);
+      if (ev_wait(C->ev[pb])) rc = REDSET_FAILURE;
+      for (int x = encode ? d : 0; x < ncell && !rc; ++x) {
+        for (size_t q = 0; q < (size_t) world && q * W < len && !rc; ++q) {
+          const size_t lo = q * W, k = min_sz(W, len - lo);
+          if (x < d) {
+            if (io_write(lofi, x, off + lo, k, HOST_SLICE(pb, x, q)) != 0) rc = fail("lofi write failed");
+          } else if (pwrite_full(fd_chunk, HOST_SLICE(pb, x, q), k,
+                                 header + (off_t) (x - d) * (off_t) chunk_size + (off_t) (off + lo)) != 0) {
+            rc = fail("write %s failed", chunk_file);
+          }
+        }
+      }
+    }
+  }
+#undef WIN_LEN
+#undef HOST_SLICE
+  return slot_done(X, C, rc);
+}
+
+/* The encode (encode = 1: every member's data cells in, its parity cells
+ * out) or the rebuild (the lost members' cells) as the sharded plan over the
+ * communicator's transport (X: RCCL, or the _SHARDED_MPI transport; the
+ * _SHARDED_HOST mode goes to sharded_slot_host). rs == NULL: XOR (e = 1;
+ * rebuild: the root is lost[0]). */
+static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int p, int r, int e, int missing,
+                        const int* lost, int need_rebuild, const redset_hip_io* lofi, const char* chunk_file,
+                        int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B, comm_exchange* X,
+                        int mode) {
+  if (mode == REDSET_HIP_EXCHANGE_SHARDED_HOST)
+    return sharded_slot_host(encode, rs, comm, p, r, e, missing, lost, need_rebuild, lofi, chunk_file, fd_chunk,
+                             header, hrc, chunk_size, B, X);
+  const int d = p - e, ncell = p, world = p;
+  const size_t win = slot_window(SHARDED_WINDOW, chunk_size, ncell, B);
   int rc = hrc;
   if (!rc && need_rebuild && !lofi->write) rc = fail("lofi has no write callback");
   int crc = 0;
   /* the mode's transport: RCCL, or the MPI transport with device buffers */
   const int over_mpi = mode == REDSET_HIP_EXCHANGE_SHARDED_MPI;
-  slot_ctx* C = slot_ctx_get(X, over_mpi ? &X->mt_tr : &X->tr, over_mpi ? X->mt : NULL, encode, rs, p, r, e, missing,
-                             lost, need_rebuild, chunk_size, win, &crc);
+  slot_ctx* C = slot_ctx_get(X, 0, over_mpi ? &X->mt_tr : &X->tr, over_mpi ? X->mt : NULL, encode, rs, p, r, e,
+                             missing, lost, need_rebuild, chunk_size, win, &crc);
   if (!rc) rc = crc;
   if ((rc = agree_setup(comm, rc))) goto out;
 
@@ -1617,18 +1803,7 @@ static int sharded_slot(int encode, const redset_hip_rs* rs, MPI_Comm comm, int 
     }
   }
 out:;
-  /* the context serves the next call of this shape; a failed call's, or
-   * every call's with the cache off, goes */
-  const double tt = now_s();
-  if (C && C->stream && hipStreamSynchronize(C->stream) != hipSuccess && !rc) rc = fail("stream sync failed");
-  if (C && (rc || !cache_on())) {
-    slot_ctx_free(C);
-    C = NULL;
-  }
-  X->ctx = C;
-  exch_busy(X, 0);
-  g_stats.setup_seconds += now_s() - tt;
-  return rc ? REDSET_FAILURE : REDSET_SUCCESS;
+  return slot_done(X, C, rc);
 }
 
 int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missing, const int* rebuild_ranks,
@@ -1651,7 +1826,7 @@ int redset_hip_rs_decode_rank(const redset_hip_rs* rs, MPI_Comm comm, int missin
   if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
   int mode;
   comm_exchange* X = NULL;
-  if (choose_exchange(comm, p, r, 1, &mode, &X)) return REDSET_FAILURE;
+  if (choose_exchange(comm, p, r, AUTO_DECODE, &mode, &X)) return REDSET_FAILURE;
   g_last_exchange = mode;
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
                ? rs_decode_host(rs, comm, p, r, e, missing, rebuild_ranks, need_rebuild, lofi, chunk_file, fd_chunk,
@@ -1677,7 +1852,7 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
   int mode;
   comm_exchange* X = NULL;
-  if (choose_exchange(comm, p, r, 1, &mode, &X)) return REDSET_FAILURE;
+  if (choose_exchange(comm, p, r, AUTO_DECODE, &mode, &X)) return REDSET_FAILURE;
   g_last_exchange = mode;
   int rc = mode == REDSET_HIP_EXCHANGE_HOST_MPI
                ? xor_decode_host(comm, p, r, root, lofi, chunk_file, fd_chunk, header, hrc, chunk_size, B)
@@ -1686,11 +1861,11 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
   return stats_end(t0, rc);
 }
 
-/* The encodes take the host ring under AUTO (choose_exchange) and the
- * sharded plan when a sharded mode is set: every data cell's column slices
- * gathered onto the GPUs, gf_mac (or the XOR) there, the parity slices
- * returned to their holders, instead of the host ring
- * (src/redset_reedsolomon.c:329-377, src/redset_xor.c:251-285). */
+/* The encodes: the sharded plan (every data cell's column slices gathered
+ * onto the GPUs, gf_mac (or the XOR) there, the parity slices returned to
+ * their holders) under a sharded mode and, over host slabs, under AUTO for RS
+ * with e >= 2; else the host ring (src/redset_reedsolomon.c:329-377,
+ * src/redset_xor.c:251-285). */
 static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_io* lofi, const char* chunk_file,
                        int fd_chunk, size_t chunk_size, size_t buf_size) {
   int p, r, e = 1;
@@ -1707,7 +1882,8 @@ static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_
   if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
   int mode;
   comm_exchange* X = NULL;
-  if (choose_exchange(comm, p, r, 0, &mode, &X)) return REDSET_FAILURE;
+  if (choose_exchange(comm, p, r, rs && e >= 2 ? AUTO_ENCODE_SLABS : AUTO_ENCODE_HOST, &mode, &X))
+    return REDSET_FAILURE;
   g_last_exchange = mode;
   int rc;
   if (mode == REDSET_HIP_EXCHANGE_HOST_MPI) {

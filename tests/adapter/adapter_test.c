@@ -108,6 +108,7 @@ static int exchange_mode(const char* s) {
   return strcmp(s, "host") == 0 ? REDSET_HIP_EXCHANGE_HOST_MPI
          : strcmp(s, "sharded-mpi") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_MPI
          : strcmp(s, "rccl") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_RCCL
+         : strcmp(s, "sharded-host") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_HOST
                                   : REDSET_HIP_EXCHANGE_AUTO;
 }
 
@@ -115,6 +116,7 @@ static const char* exchange_name(int m) {
   return m == REDSET_HIP_EXCHANGE_HOST_MPI ? "host"
          : m == REDSET_HIP_EXCHANGE_SHARDED_MPI ? "sharded-mpi"
          : m == REDSET_HIP_EXCHANGE_SHARDED_RCCL ? "rccl"
+         : m == REDSET_HIP_EXCHANGE_SHARDED_HOST ? "sharded-host"
                                                  : "none";
 }
 
@@ -190,7 +192,7 @@ int main(int argc, char** argv) {
     if (fd < 0 || lseek(fd, (off_t) header, SEEK_SET) < 0) MPI_Abort(MPI_COMM_WORLD, 5);
   }
 
-  /* ADAPTER_TEST_EXCHANGE=host|sharded-mpi|rccl: the rebuild's exchange
+  /* ADAPTER_TEST_EXCHANGE=host|sharded-mpi|sharded-host|rccl: the rebuild's exchange
    * (include/redset_hip_mpi.h; default auto, which takes the host path when
    * the members share the box's one GPU) */
   const char* ex = getenv("ADAPTER_TEST_EXCHANGE");

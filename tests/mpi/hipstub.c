@@ -111,7 +111,10 @@ int redset_hip_rs_decode_matrix(const redset_hip_rs* rs, int missing, const int*
 enum { STUB_RS_ENCODE = 1, STUB_RS_REBUILD = 2, STUB_XOR_ENCODE = 3, STUB_XOR_REBUILD = 4 };
 struct redset_hip_plan {
   int kind, p, e, missing, lost[256];
-  const redset_hip_rs* rs;
+  /* the coefficients, copied at plan time as the library's plans do (the
+   * caller may destroy its codec while the plan lives): the encoding matrix,
+   * or every stripe's decode map */
+  unsigned char* coef;
   unsigned char **lofi, **par;
   size_t n, stride;
 };
@@ -121,8 +124,15 @@ static int stub_plan(int kind, const redset_hip_rs* rs, int p, int e, int missin
                      struct redset_hip_plan** out) {
   struct redset_hip_plan* P = calloc(1, sizeof(*P));
   if (!P) return 1;
-  P->kind = kind, P->rs = rs, P->p = p, P->e = e, P->missing = missing, P->n = n, P->stride = stride;
+  P->kind = kind, P->p = p, P->e = e, P->missing = missing, P->n = n, P->stride = stride;
   for (int i = 0; i < missing; ++i) P->lost[i] = lost[i];
+  if (kind == STUB_RS_ENCODE) {
+    P->coef = malloc((size_t) (p + e) * p);
+    redset_hip_rs_matrix(rs, P->coef);
+  } else if (kind == STUB_RS_REBUILD) {
+    P->coef = malloc((size_t) p * missing * p);
+    for (int c = 0; c < p; ++c) redset_hip_rs_decode_matrix(rs, missing, lost, c, P->coef + (size_t) c * missing * p);
+  }
   P->lofi = malloc(sizeof(*P->lofi) * (size_t) p);
   P->par = malloc(sizeof(*P->par) * (size_t) p);
   for (int r = 0; r < p; ++r) P->lofi[r] = lofi[r], P->par[r] = par[r];
@@ -153,6 +163,7 @@ int redset_hip_xor_plan_rebuild(int p, int root, unsigned char* const* lofi, uns
 }
 void redset_hip_plan_destroy(struct redset_hip_plan* P) {
   if (!P) return;
+  free(P->coef);
   free(P->lofi);
   free(P->par);
   free(P);
@@ -170,9 +181,7 @@ static unsigned char* stub_cell(const struct redset_hip_plan* P, int r, int c) {
 int redset_hip_plan_execute(const struct redset_hip_plan* P, void* stream) {
   (void) stream;
   const int p = P->p, e = P->e;
-  unsigned char* mat = malloc((size_t) (p + e) * p);
-  unsigned char* D = malloc((size_t) (P->missing ? P->missing : 1) * p);
-  if (P->rs && P->kind == STUB_RS_ENCODE) redset_hip_rs_matrix(P->rs, mat);
+  const unsigned char* mat = P->coef;
   for (int c = 0; c < p; ++c) {
     if (P->kind == STUB_RS_ENCODE) { /* parity slot i of stripe c = row p + i over its data holders */
       for (int r = 0; r < p; ++r) {
@@ -188,7 +197,7 @@ int redset_hip_plan_execute(const struct redset_hip_plan* P, void* stream) {
         }
       }
     } else if (P->kind == STUB_RS_REBUILD) {
-      redset_hip_rs_decode_matrix(P->rs, P->missing, P->lost, c, D);
+      const unsigned char* D = P->coef + (size_t) c * P->missing * p;
       for (int i = 0; i < P->missing; ++i) {
         unsigned char* out = stub_cell(P, P->lost[i], c);
         memset(out, 0, P->n);
@@ -210,7 +219,5 @@ int redset_hip_plan_execute(const struct redset_hip_plan* P, void* stream) {
       }
     }
   }
-  free(mat);
-  free(D);
   return 0;
 }

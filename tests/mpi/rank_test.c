@@ -9,7 +9,7 @@
  * Rank r reads <dir>/manifest_<r>.txt:
  *   nfiles \n path size \n ... chunk_size \n header_size \n redundancy_path
  * (written by tests/test_gpu_mpi.py). Exit 0 iff every rank succeeded.
- * RANK_TEST_EXCHANGE=host|sharded-mpi|rccl: the rebuild's exchange
+ * RANK_TEST_EXCHANGE=host|sharded-mpi|sharded-host|rccl: the rebuild's exchange
  * (redset_hip_rank_set_exchange; default auto). Rank 0 prints the one used.
  * RANK_TEST_DEVICE_PER_RANK=1: rank r on GPU r mod (GPUs).
  * RANK_TEST_FAIL_READ=<rank>: that rank's logical-file reads fail from the
@@ -59,6 +59,7 @@ static int exchange_mode(const char* s) {
   return strcmp(s, "host") == 0 ? REDSET_HIP_EXCHANGE_HOST_MPI
          : strcmp(s, "sharded-mpi") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_MPI
          : strcmp(s, "rccl") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_RCCL
+         : strcmp(s, "sharded-host") == 0 ? REDSET_HIP_EXCHANGE_SHARDED_HOST
                                   : REDSET_HIP_EXCHANGE_AUTO;
 }
 
@@ -66,6 +67,7 @@ static const char* exchange_name(int m) {
   return m == REDSET_HIP_EXCHANGE_HOST_MPI ? "host"
          : m == REDSET_HIP_EXCHANGE_SHARDED_MPI ? "sharded-mpi"
          : m == REDSET_HIP_EXCHANGE_SHARDED_RCCL ? "rccl"
+         : m == REDSET_HIP_EXCHANGE_SHARDED_HOST ? "sharded-host"
                                                  : "none";
 }
 

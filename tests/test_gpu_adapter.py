@@ -39,7 +39,7 @@ def _need():
     assert os.path.exists(DRIVER), f"{DRIVER} missing: build it with `make -C tests/adapter` (needs the reference headers)"
 
 
-@pytest.mark.parametrize("exchange", ["auto", "sharded-mpi"])
+@pytest.mark.parametrize("exchange", ["auto", "sharded-mpi", "sharded-host"])
 @pytest.mark.parametrize("scheme,p,e,lost,buf,repeat", [
     ("rs", 4, 2, [1, 2], 65536, 1),
     ("rs", 4, 2, [0, 3], 1 << 20, 2),   # the second call reuses the adapter's cached codec
@@ -50,11 +50,12 @@ def _need():
 def test_adapter_slot_encode_and_rebuild(oracle, tmp_path, scheme, p, e, lost, buf, repeat, exchange):
     """Encode, lose members, rebuild through the reference-signature slot.
     exchange "auto": on the box's one GPU the members share a device, so the
-    rebuild takes the host-MPI path; "sharded-mpi": the path redset_recover()
-    takes when every member owns a GPU -- the sharded plan (column slices
-    gathered onto every GPU, gf_mac, rebuilt slices returned) -- over the
-    MPI transport with device buffers in place of RCCL (RCCL needs one GPU
-    per rank)."""
+    rebuild takes the host-MPI path (and an RS encode with e >= 2 the host
+    slabs); "sharded-mpi": the path redset_recover() takes when every member
+    owns a GPU -- the sharded plan (column slices gathered onto every GPU,
+    gf_mac, rebuilt slices returned) -- over the MPI transport with device
+    buffers in place of RCCL (RCCL needs one GPU per rank); "sharded-host":
+    the same plan over slabs in page-locked host memory."""
     _need()
     tmp = str(tmp_path)
     d = p - e

@@ -45,23 +45,32 @@ def _mpirun(np_, args, timeout=300, env=None):
 # RCCL over xGMI when every member owns a GPU of one node -- on the test box
 # the members share one GPU, so auto must take the host path --, and
 # "sharded-mpi" runs the same sharded plan (gather column slices, gf_mac on
-# every GPU, return) over the MPI transport with device buffers
-EXCHANGES = ["auto", "sharded-mpi", "sharded-mpi-windows"]
+# every GPU, return) over the MPI transport with device buffers, and
+# "sharded-host" over slabs in page-locked host memory (the kernels read and
+# write them in place; rank_mpi.c sharded_slot_host)
+EXCHANGES = ["auto", "sharded-mpi", "sharded-mpi-windows", "sharded-host", "sharded-host-windows"]
 TWIN_DIR = os.path.join(ROOT, "redset_amd", "lib_test")
 
 
 def _exchange_env(exchange):
-    if exchange == "sharded-mpi-windows":
+    if exchange.endswith("-windows"):
         # the test twin (loaded ahead of the driver's RUNPATH) with 64 KiB
-        # windows: small sets take several windows, double-buffered
+        # windows: small sets take several windows
         ld = os.environ.get("LD_LIBRARY_PATH")
-        return {"RANK_TEST_EXCHANGE": "sharded-mpi", "REDSET_HIP_TEST_SHARDED_WINDOW": "65536",
+        return {"RANK_TEST_EXCHANGE": exchange[:-len("-windows")], "REDSET_HIP_TEST_SHARDED_WINDOW": "65536",
                 "LD_LIBRARY_PATH": TWIN_DIR + (":" + ld if ld else "")}
     return {"RANK_TEST_EXCHANGE": exchange}
 
 
-def _check_exchange(res, exchange, op="rebuild"):
-    used = "host" if exchange == "auto" else exchange.replace("-windows", "")
+def _auto_exchange(op, scheme, e):
+    """what AUTO picks on the test box (its members share one GPU): the host
+    path, but an RS encode with e >= 2 over host slabs (rank_mpi.c
+    choose_exchange, AUTO_ENCODE_SLABS)"""
+    return "sharded-host" if op == "encode" and scheme == "rs" and e >= 2 else "host"
+
+
+def _check_exchange(res, exchange, op="rebuild", scheme="rs", e=2):
+    used = _auto_exchange(op, scheme, e) if exchange == "auto" else exchange.replace("-windows", "")
     assert f"{op} exchange {used}" in res.stdout, res.stdout
 
 
@@ -113,7 +122,7 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf, exchange):
 
     res = _mpirun(p, [scheme, "encode", e, tmp, buf], env=_exchange_env(exchange))
     assert res.returncode == 0, res.stdout + res.stderr
-    _check_exchange(res, exchange, "encode")
+    _check_exchange(res, exchange, "encode", scheme, e)
     lofi = [_logical(fl, d * chunk) for fl in files]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     if scheme == "rs":
@@ -174,6 +183,13 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf, exchange):
                       "REDSET_HIP_TEST_SHARDED_WINDOW": "65536"}),
     ("xor", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "3", "RANK_TEST_EXCHANGE": "sharded-mpi",
                        "REDSET_HIP_TEST_SHARDED_WINDOW": "65536"}),
+    # the same over host slabs
+    ("rs", "rebuild", {"RANK_TEST_FAIL_READ": "3", "RANK_TEST_EXCHANGE": "sharded-host"}),
+    ("rs", "encode", {"RANK_TEST_FAIL_READ": "2", "RANK_TEST_EXCHANGE": "sharded-host"}),
+    ("rs", "encode", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "1", "RANK_TEST_EXCHANGE": "sharded-host",
+                      "REDSET_HIP_TEST_SHARDED_WINDOW": "65536"}),
+    ("xor", "rebuild", {"REDSET_HIP_INJECT_DEVICE_FAILURE": "3", "RANK_TEST_EXCHANGE": "sharded-host",
+                        "REDSET_HIP_TEST_SHARDED_WINDOW": "65536"}),
 ])
 def test_mpi_rank_failure_fails_every_rank_without_hang(oracle, tmp_path, scheme, op, env):
     """One member's I/O or device error in the middle of the loop: that member
@@ -258,7 +274,7 @@ def test_mpi_config0_xor_4_ranks_16MiB(oracle, tmp_path, exchange):
     _manifests(tmp, files, chunk, header, reds)
     res = _mpirun(p, ["xor", "encode", e, tmp, 1 << 20], env=_exchange_env(exchange))
     assert res.returncode == 0, res.stdout + res.stderr
-    _check_exchange(res, exchange, "encode")
+    _check_exchange(res, exchange, "encode", "xor", e)
     lofi = [_logical(fl, (p - 1) * chunk) for fl in files]
     want = [np.zeros(chunk, np.uint8) for _ in range(p)]
     oracle.xor_encode_set(p, lofi, want, chunk)
@@ -319,7 +335,7 @@ def test_mpi_rank_backends_repeated_calls(oracle, tmp_path, scheme, p, e, lost, 
     cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST, scheme, "encode", str(e), tmp, "32768"]
     res = run_group(cmd, 120, env=env)
     assert res.returncode == 0 and "call 3 of 3" in res.stdout, res.stdout + res.stderr
-    _check_exchange(res, exchange, "encode")
+    _check_exchange(res, exchange, "encode", scheme, e)
     lofi = [_logical(fl, d * chunk) for fl in files]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     if scheme == "rs":
@@ -365,10 +381,10 @@ def test_mpi_rank_backends_random(oracle, tmp_path, seed):
     reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
     _manifests(tmp, files, chunk, header, reds)
     crcs = {path: oracle.crc32(np.fromfile(path, dtype=np.uint8)) for fl in files for path, _ in fl}
-    exchange = EXCHANGES[seed % 3]
+    exchange = EXCHANGES[seed % len(EXCHANGES)]
     res = _mpirun(p, [scheme, "encode", e, tmp, buf], timeout=120, env=_exchange_env(exchange))
     assert res.returncode == 0, (scheme, p, e, buf, exchange, res.stdout + res.stderr)
-    _check_exchange(res, exchange, "encode")
+    _check_exchange(res, exchange, "encode", scheme, e)
     lofi = [_logical(fl, d * chunk) for fl in files]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     if scheme == "rs":
@@ -451,7 +467,7 @@ def test_mpi_xor_decode_orders(oracle, tmp_path, order, p, lost, buf):
     assert np.array_equal(np.fromfile(reds[lost], dtype=np.uint8)[header[lost]:], want)
 
 
-@pytest.mark.parametrize("exchange", ["auto", "sharded-mpi"])
+@pytest.mark.parametrize("exchange", ["auto", "sharded-mpi", "sharded-host"])
 def test_mpi_rs_slices_larger_than_the_buffer(oracle, tmp_path, exchange):
     """~20 MB chunks with a 64 KiB buffer: the RS backends move slices of
     chunk/16 (rank_mpi.c slice_bytes) and the encode stages whole ring
@@ -486,8 +502,9 @@ def test_mpi_rs_slices_larger_than_the_buffer(oracle, tmp_path, exchange):
         assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[4096:], want[r]), r
 
 
+@pytest.mark.parametrize("exchange", ["sharded-mpi", "sharded-host"])
 @pytest.mark.parametrize("scheme,op", [("rs", "encode"), ("rs", "rebuild")])
-def test_mpi_hang_cap_fails_the_call(oracle, tmp_path, scheme, op):
+def test_mpi_hang_cap_fails_the_call(oracle, tmp_path, scheme, op, exchange):
     """The fault contract through the drop-in slot (include/redset_hip.h
     redset_hip_hang_faults): the sharded exchange's plans forced into streamed
     pairs (test twin, REDSET_HIP_SEQUENTIAL=3) with a loader that sleeps
@@ -507,7 +524,7 @@ def test_mpi_hang_cap_fails_the_call(oracle, tmp_path, scheme, op):
     reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
     _manifests(tmp, files, chunk, [512] * p, reds)
     ld = os.environ.get("LD_LIBRARY_PATH")
-    stall = {"RANK_TEST_EXCHANGE": "sharded-mpi", "REDSET_HIP_SEQUENTIAL": "3",
+    stall = {"RANK_TEST_EXCHANGE": exchange, "REDSET_HIP_SEQUENTIAL": "3",
              "REDSET_HIP_TEST_TABLE_DELAY": "400", "LD_LIBRARY_PATH": TWIN_DIR + (":" + ld if ld else "")}
     args = [scheme, "encode", e, tmp, 16384]
     if op == "rebuild":
@@ -536,7 +553,7 @@ def test_mpi_hang_cap_fails_the_call(oracle, tmp_path, scheme, op):
 @pytest.mark.parametrize("scheme,p,e,lost", [("rs", 4, 2, [1, 3]), ("xor", 3, 1, [2])])
 def test_mpi_auto_rebuild_takes_rccl_with_a_gpu_per_member(oracle, tmp_path, scheme, p, e, lost):
     """AUTO's production layout: members on one node, each on its
-    own GPU. The encode stays on the host ring; the rebuild must take the
+    own GPU. The encode stays off RCCL (host ring or host slabs); the rebuild must take the
     RCCL exchange (rank_mpi.c choose_exchange) and restore the lost members
     bit for bit. Needs >= p GPUs: the one-GPU test box skips it, a node with
     8 GPUs runs it (src/redset_reedsolomon.c:646-733 replaced)."""
@@ -556,7 +573,7 @@ def test_mpi_auto_rebuild_takes_rccl_with_a_gpu_per_member(oracle, tmp_path, sch
     env = {"RANK_TEST_DEVICE_PER_RANK": "1"}
     res = _mpirun(p, [scheme, "encode", e, tmp, 1 << 20], env=env)
     assert res.returncode == 0, res.stdout + res.stderr
-    assert "encode exchange host" in res.stdout, res.stdout
+    assert f"encode exchange {_auto_exchange('encode', scheme, e)}" in res.stdout, res.stdout
     for r in lost:
         for path, _ in files[r]:
             os.unlink(path)

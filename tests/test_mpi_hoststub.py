@@ -213,7 +213,7 @@ def test_host_path_xor_decode_orders(stub, oracle, tmp_path, order, p, lost, buf
     assert got == (p if order == "chain" else (p - 1) * p) * chunk, (got, chunk)
 
 
-@pytest.mark.parametrize("exchange", ["host", "sharded-mpi"])
+@pytest.mark.parametrize("exchange", ["host", "sharded-mpi", "sharded-host"])
 @pytest.mark.parametrize("scheme,op,rank", [("rs", "encode", 1), ("rs", "rebuild", 3), ("xor", "encode", 0),
                                              ("xor", "rebuild", 2)])
 def test_hang_capped_kernel_wait_fails_the_call(stub, oracle, tmp_path, scheme, op, rank, exchange):
@@ -254,22 +254,26 @@ TWIN_DIR = os.path.join(ROOT, "redset_amd", "lib_test")
 
 @pytest.mark.parametrize("scheme,p,e,lost,window", [("rs", 6, 2, [1, 4], 0), ("rs", 5, 3, [0, 2, 4], 0),
                                                      ("xor", 4, 1, [2], 0), ("rs", 4, 2, [0, 3], 65536),
-                                                     ("xor", 5, 1, [0], 40000)])
-def test_sharded_slot_round_trip(stub, oracle, tmp_path, scheme, p, e, lost, window):
-    """The per-rank backends' sharded exchange (rank_mpi.c sharded_slot: the
-    RCCL path's plan, here over the MPI transport with device buffers) on the
-    CPU: the HIP stand-in also runs the whole-set plans the sharded plan
-    computes with, so the slot's windows, planning, transport reserve,
-    staging and exchanges run end to end, encode and rebuild, checked against
-    the oracle. window > 0: the test twin with windows of that many bytes, so
-    a set takes several (double-buffered, a tail window)."""
-    env = {"RANK_TEST_EXCHANGE": "sharded-mpi", "RANK_TEST_REPEAT": "2"}
+                                                     ("xor", 5, 1, [0], 40000), ("rs", 7, 3, [2, 5, 6], 5000)])
+@pytest.mark.parametrize("exchange", ["sharded-mpi", "sharded-host"])
+def test_sharded_slot_round_trip(stub, oracle, tmp_path, scheme, p, e, lost, window, exchange):
+    """The per-rank backends' sharded exchange on the CPU: the HIP stand-in
+    also runs the whole-set plans the sharded plan computes with, so the
+    slot's windows, planning, transport reserve, staging and exchanges run end
+    to end, encode and rebuild, checked against the oracle. "sharded-mpi":
+    rank_mpi.c sharded_slot, the RCCL path's slot over the MPI transport with
+    device buffers; "sharded-host": sharded_slot_host, every slab in pinned
+    host memory (slice-by-slice reads and writes, no staging). window > 0: the
+    test twin with windows of that many bytes, so a set takes several
+    (double-buffered, a tail window; 5000-B windows cut ragged slices)."""
+    env = {"RANK_TEST_EXCHANGE": exchange, "RANK_TEST_REPEAT": "2"}
     if window:
         env["REDSET_HIP_TEST_SHARDED_WINDOW"] = str(window)
         env["LD_LIBRARY_PATH"] = TWIN_DIR + (":" + os.environ["LD_LIBRARY_PATH"] if os.environ.get("LD_LIBRARY_PATH")
                                                else "")
     enc, reb, chunk = _round_trip(oracle, str(tmp_path), scheme, p, e, lost, 32768, 900 + p, 300_000, env=env)
-    assert "encode exchange sharded-mpi" in enc.stdout, enc.stdout
+    assert f"encode exchange {exchange}" in enc.stdout, enc.stdout
+    assert f"rebuild exchange {exchange}" in reb.stdout, reb.stdout
     classes = ["read_seconds", "mpi_seconds", "gpu_seconds", "write_seconds", "stage_seconds", "copy_seconds",
                "plan_seconds", "setup_seconds"]
     for res in (enc, reb):
@@ -284,11 +288,12 @@ def test_sharded_slot_round_trip(stub, oracle, tmp_path, scheme, p, e, lost, win
         assert first["plan_seconds"][0] > 0 and warm["plan_seconds"][1] == 0, (first, warm)
 
 
-def test_sharded_slot_without_the_cache_plans_every_call(stub, oracle, tmp_path):
+@pytest.mark.parametrize("exchange", ["sharded-mpi", "sharded-host"])
+def test_sharded_slot_without_the_cache_plans_every_call(stub, oracle, tmp_path, exchange):
     """REDSET_HIP_SCRATCH_CACHE=0: the slot context goes with every call (as the
     reference allocates per call, src/redset_reedsolomon.c:298-302), so the
     second call plans again -- and is still bit-exact."""
-    env = {"RANK_TEST_EXCHANGE": "sharded-mpi", "RANK_TEST_REPEAT": "2", "REDSET_HIP_SCRATCH_CACHE": "0"}
+    env = {"RANK_TEST_EXCHANGE": exchange, "RANK_TEST_REPEAT": "2", "REDSET_HIP_SCRATCH_CACHE": "0"}
     enc, reb, _ = _round_trip(oracle, str(tmp_path), "rs", 5, 2, [1, 3], 32768, 77, 200_000, env=env)
     for res in (enc, reb):
         assert _stats(res.stdout, "warm")["plan_seconds"][0] > 0, res.stdout

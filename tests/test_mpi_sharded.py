@@ -120,13 +120,17 @@ def _rank_test_set(tmp, p, chunk):
 
 
 @pytest.mark.parametrize("op", ["rebuild", "encode"])
-@pytest.mark.parametrize("exchange,used", [("", "host"), ("host", "host"), ("sharded-mpi", "sharded-mpi")])
+@pytest.mark.parametrize("exchange,used", [("", None), ("host", "host"), ("sharded-mpi", "sharded-mpi"),
+                                           ("sharded-host", "sharded-host")])
 def test_rebuild_exchange_choice_on_cpu(tmp_path, exchange, used, op):
-    """The per-rank decode's exchange choice (rank_mpi.c choose_exchange) is
+    """The per-rank backends' exchange choice (rank_mpi.c choose_exchange) is
     collective and agreed before any exchange: on a machine without a GPU,
-    "auto" finds no GPU per member and takes the host path, a forced mode is
-    taken as asked, and the decode then fails on every member (no HIP device)
-    without a hang. The GPU tests run the same choices to completion."""
+    "auto" finds no GPU per member and takes the host path for the decode
+    (and, RS(2+2) here, the host slabs for the encode), a forced mode is taken
+    as asked, and the call then fails on every member (no HIP device) without
+    a hang. The GPU tests run the same choices to completion."""
+    if used is None:
+        used = "sharded-host" if op == "encode" else "host"
     if not _have() or not os.path.exists(RANK_TEST):
         pytest.skip("needs MPICH and tests/mpi/build/rank_test")
     from conftest import gpu_available

@@ -6,7 +6,8 @@
 #          rehearsals' callback transport pays; tools/gloo_p2p_probe.py)
 #   n2     bench.py --gpus 2 rehearsal over gloo on the one GPU
 #   rank   the per-rank slot's roofline (tools/rank_bench.py): RS(8+3) 64 MiB
-#          and configs[0] (XOR, 4 x 16 MiB files), host and sharded exchange
+#          and configs[0] (XOR, 4 x 16 MiB files), host and sharded exchanges
+#          (RANK_EXCHANGES, default "host sharded-mpi sharded-host")
 #   wide   RS(16+4) (configs[4]'s stripe) device-resident: kernel stats, PMC
 #          FETCH/WRITE and SQ counters
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -35,7 +36,7 @@ for probe in "$@"; do
         --master-port 29543 bench.py --gpus 2 --dist-backend gloo --chunk-mib 2 --steps 3 --warmup 1 \
         --cpu-baseline 0 --pairs 0 ;;
     rank)
-      for ex in host sharded-mpi; do
+      for ex in ${RANK_EXCHANGES:-host sharded-mpi sharded-host}; do
         run rank_rs_64m_$ex 400 python tools/rank_bench.py --ranks 11 --encoding 3 --chunk-mib 64 --buf-mib 16 \
           --repeat 5 --exchange $ex --dir /tmp/rank_bench_$ex
         run rank_config0_$ex 200 python tools/rank_bench.py --scheme xor --ranks 4 --file-bytes 16777216 \

@@ -70,7 +70,7 @@ def main():
     ap.add_argument("--lost", default="1,2")
     ap.add_argument("--dir", default="/tmp/rank_bench")
     ap.add_argument("--repeat", type=int, default=1, help="calls per process; the median of calls 2..N is reported as warm")
-    ap.add_argument("--exchange", default="auto", help="rebuild exchange: auto, host, sharded-mpi, rccl")
+    ap.add_argument("--exchange", default="auto", help="exchange: auto, host, sharded-mpi, sharded-host, rccl")
     ap.add_argument("--pcie-gbps", type=float, default=55.0,
                     help="PCIe DMA ceiling per direction (profiles/r01_pcie_probe.json: 55-56 GB/s H2D)")
     a = ap.parse_args()

@@ -23,7 +23,9 @@ peers spreads over p - 1 links. This is the model the first
 redset_recover() on such a node is to be read against
 (redset_hip_rank_last_stats gives the measured side).
 
-usage: python tools/slot_model.py [--chunk-mib 64] -> one JSON line per case
+usage: python tools/slot_model.py [--chunk-mib 64] [--network] -> one JSON line per case
+(--network: the encode's bytes per member with a node per member, the
+reference's ring against the sharded plan, network_encode)
 """
 import argparse
 import ctypes
@@ -128,11 +130,53 @@ def model(scheme, p, e, lost, chunk, op):
     }
 
 
+NIC_GBPS = 25.0  # a 200 Gb/s NIC per node and direction: an assumption, not measured here
+
+
+def network_encode(p, e, chunk):
+    """The encode's network bytes per member with every member on its own
+    node (redset's usual placement): the reference's ring, which the host
+    exchange keeps, sends each of a member's d data cells to the e parity
+    holders of its stripe and receives as much (src/redset_reedsolomon.c:
+    329-363: d ring steps x e sends of one segment), d*e cells each way; the
+    sharded plan over host slabs (rank_mpi.c sharded_slot_host, AUTO for RS
+    encodes with e >= 2) sends the column slices the C planner lists."""
+    from redset_amd import _lib as L
+
+    lib = L.load()
+    rs = c_void_p()
+    lib.redset_hip_rs_create(p, e, ctypes.byref(rs))
+    d = p - e
+    sent = recv = 0
+    for r in range(p):
+        inf = plan_info(L, lib, rs, p, e, L.PLAN_RS_ENCODE, [], chunk, r)
+        sent = max(sent, inf["gather_bytes_sent"] + inf["return_bytes_sent"])
+        recv = max(recv, inf["gather_bytes_recv"] + inf["return_bytes_recv"])
+    lib.redset_hip_rs_destroy(rs)
+    ring = d * e * chunk
+    sharded = max(sent, recv)
+    return {
+        "case": f"RS({d}+{e}) p={p} encode, chunk {chunk >> 20} MiB, a node per member",
+        "ring_bytes_per_member_each_way": ring,
+        "sharded_bytes_per_member_each_way": {"sent": sent, "recv": recv},
+        "cells_each_way": {"ring": d * e, "sharded": round(sharded / chunk, 3)},
+        "ratio_ring_over_sharded": round(ring / sharded, 3),
+        "seconds_at_nic": {"ring": round(ring / (NIC_GBPS * 1e9), 4), "sharded": round(sharded / (NIC_GBPS * 1e9), 4)},
+        "nic_GBps_per_direction": NIC_GBPS,
+    }
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--chunk-mib", type=int, default=64)
+    ap.add_argument("--network", action="store_true",
+                    help="the encode's network bytes with a node per member: ring vs sharded plan")
     a = ap.parse_args()
     C = a.chunk_mib << 20
+    if a.network:
+        for p, e in [(4, 2), (6, 2), (8, 3), (11, 3), (10, 2), (20, 4)]:
+            print(json.dumps(network_encode(p, e, C)))
+        return
     for scheme, p, e, lost, op in [("rs", 8, 3, [1, 2], "rebuild"), ("rs", 8, 2, [1, 2], "rebuild"),
                                    ("rs", 8, 3, [], "encode"), ("xor", 8, 1, [3], "rebuild")]:
         print(json.dumps(model(scheme, p, e, lost, C, op)))

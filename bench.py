@@ -500,6 +500,10 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
         },
     }
     out.update(runner.report(s_step, "rebuild"))
+    # the plans, the codec and the RCCL communicator go before the process
+    # group does (every rank is past the same collectives here)
+    torch.cuda.synchronize()
+    runner.close()
     return out
 
 

@@ -418,6 +418,8 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
 
     import redset_amd
     from redset_amd import dist as rdist
+    from redset_amd._lib import PHASE_COMPUTE as L_PHASE_COMPUTE, PHASE_GATHER as L_PHASE_GATHER
+    from redset_amd._lib import PHASE_RETURN as L_PHASE_RETURN
 
     dist_on = world > 1
     dev = "cuda" if (not dist_on or dist.get_backend() == "nccl") else "cpu"
@@ -450,6 +452,15 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     timed(lambda i: runner.rebuild(), 3, 1, dist_on, before=runner.reset_timing)
     phases = runner.phase_ms()
     compute_ms = phases.get("rebuild_gathered->computed")
+    # BASELINE.md's C4 as it states it: the column-sharded decode on N GPUs
+    # with every GPU's slices already in place, and the RCCL exchange (gather
+    # + return) timed separately -- each K steps bracketed like the step,
+    # max over ranks
+    d_step = timed(lambda i: runner.run_phases("rebuild", [L_PHASE_COMPUTE]), args.steps, args.warmup,
+                   dist_on) / args.steps
+    x_step = timed(lambda i: runner.run_phases("rebuild", [L_PHASE_GATHER, L_PHASE_RETURN]), args.steps,
+                   args.warmup, dist_on) / args.steps
+    decode_value = world * runner.algorithmic_bytes("rebuild") / d_step / 1e9
     # The step's roofline is the fabric, not HBM: every GPU sends its
     # share of the decode inputs' slices to every other GPU and gets the
     # rebuilt slices back (an all-to-all over the node's fully connected
@@ -488,6 +499,20 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s (algorithmic bytes / step time)",
             "frac": round(runner.algorithmic_bytes("rebuild") / s_step / 1e9 / HBM_PEAK_GBPS, 4),
+        },
+        # C4's decode alone, slices in place (all GPUs, max over ranks)
+        "decode": {
+            "value": round(decode_value, 2),
+            "unit": "GB/s",
+            "frac_of_hbm": round(decode_value / (world * HBM_PEAK_GBPS), 6),
+            "ms_per_step": round(d_step * 1e3, 4),
+            "note": "the rebuild's gf_mac on every GPU's column slice, inputs already gathered (no exchange)",
+        },
+        # C4's RCCL exchange alone: gather + return (no compute)
+        "exchange_only": {
+            "ms_per_step": round(x_step * 1e3, 4),
+            "send_GBps_per_gpu": round(sent_mean / x_step / 1e9, 2) if sent_mean else None,
+            "frac_of_xgmi": round(sent_mean / x_step / 1e9 / link_peak, 4) if (sent_mean and dist_on) else None,
         },
         # HBM is the bound of the compute phase alone (phased diagnostic)
         "compute_hbm": {
@@ -708,8 +733,10 @@ def main():
             # which number is which: `value` is the independent-sets step
             # (configs[2] + configs[3] on each GPU), comparable from N=1 to
             # N=8; configs[3]'s multi-GPU scaling curve is sharded.value
-            "scaling_value": ("sharded.value: configs[3]'s column-sharded rebuild over RCCL/xGMI, "
-                              "with sharded.frac_of_hbm" if args.sharded else None),
+            "scaling_value": ("sharded.value: configs[3]'s column-sharded rebuild step over RCCL/xGMI "
+                              "(gather + gf_mac + return, pipelined over the sets), with sharded.frac_of_hbm; "
+                              "sharded.decode and sharded.exchange_only: its decode on slices in place and its "
+                              "RCCL exchange timed apart (BASELINE.md C4)" if args.sharded else None),
         },
     }
     step_ms = sorted(ev[k][0].elapsed_time(ev[k][2]) for k in range(args.steps))

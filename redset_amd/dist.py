@@ -292,6 +292,17 @@ class ShardedSetRunner:
         _lib.check(L.redset_hip_sharded_execute_phase(h, _lib.PHASE_RETURN, stream), f"sharded {op} return")
         self._mark(f"{op}_done")
 
+    def run_phases(self, op: str, phases) -> None:
+        """Only the given phases of one execute (redset_hip_sharded_execute_phase),
+        in order, with no marks: the bench times the decode on slices already in
+        place (PHASE_COMPUTE) and the exchange (PHASE_GATHER, PHASE_RETURN) apart,
+        as BASELINE.md's C4 asks."""
+        L = _lib.load()
+        h = self._plans[op]
+        stream = torch.cuda.current_stream().cuda_stream if self.device.type == "cuda" else None
+        for ph in phases:
+            _lib.check(L.redset_hip_sharded_execute_phase(h, ph, stream), f"sharded {op} phase {ph}")
+
     def encode(self) -> None:
         """Parity of every stripe of every set: gather data slices, compute my
         column slice, return parity slices to their hosts."""

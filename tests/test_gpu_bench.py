@@ -43,14 +43,19 @@ def _check_sharded(sh, world):
     assert sh["bit_exact"] is True
     assert sh["value"] > 0 and 0 < sh["frac_of_hbm"] < 1  # gloo moves tens of MB/s: a tiny fraction
     assert sh["hbm_peak_GBps"] == world * 8000.0
+    # the decode on slices in place and the exchange, timed apart
+    assert sh["decode"]["value"] > 0 and 0 < sh["decode"]["frac_of_hbm"] < 1, sh["decode"]
+    assert sh["exchange_only"]["ms_per_step"] >= 0
     msgs = sh["exchange"]["messages_per_gpu"]["rebuild"]
     if world > 1:
         # every GPU gathers slices from its peer and returns rebuilt slices
         assert msgs["gather_messages"] > 0 and msgs["return_messages"] > 0, msgs
         assert sh["exchange"]["bytes_sent_per_gpu_per_step"] > 0
+        assert sh["exchange_only"]["send_GBps_per_gpu"] > 0, sh["exchange_only"]
     else:
         assert msgs["gather_messages"] == 0 and msgs["return_messages"] == 0, msgs
         assert sh["roofline"]["bound"] == "hbm" and sh["exchange"]["bytes_sent_per_gpu_per_step"] == 0
+        assert sh["exchange_only"]["send_GBps_per_gpu"] is None
 
 
 @pytest.mark.timeout(420)

@@ -1,0 +1,113 @@
+#!/usr/bin/env python3
+"""What bench.py's sharded leg (configs[3]) should show at N = 1/2/4/8 on a
+node of MI355X GPUs, from the C planner itself: for every GPU g the
+rebuild plan of redset_amd/dist.py's placement (N sets of p members, member
+m of the world on GPU m mod N, each GPU's lost members last) is planned with
+a compute callback and a no-op transport, so no GPU and no process group are
+needed and nothing executes. Per GPU it reports the bytes sent and received
+over the fabric per step (redset_hip_sharded_info) and the algorithmic
+bytes of its compute, and prices them:
+
+  xgmi   max(sent, recv) / ((N - 1) x 153 GB/s): an all-to-all over the
+         fully connected mesh, one link per GPU pair
+  hbm    compute bytes / the measured gf_mac rebuild rate (6.3 TB/s,
+         profiles/r05s13_bench_kernel_stats.csv)
+
+The leg pipelines its sets (set k + 1's gather under set k's gf_mac), so a
+step costs about the larger of the two; `model_value` is then N sets'
+algorithmic rebuild bytes over that. SCALE_rNN's sharded.value at each N is
+to be read against it.
+
+usage: python tools/sharded_model.py [--chunk-mib 64] [--ranks 11] [--encoding 3] [--lost 1,2]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+from ctypes import c_int, c_void_p
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+XGMI_LINK_GBPS = 153.0
+GF_MAC_REBUILD_GBPS = 6300.0
+
+
+def placement(p, lost, world):
+    """dist.py ShardedSetRunner._place: (host, slot) of every member"""
+    where = {}
+    for g in range(world):
+        mine = [m for m in range(world * p) if m % world == g]
+        alive = [m for m in mine if (m % p) not in lost]
+        dead = [m for m in mine if (m % p) in lost]
+        for j, m in enumerate(alive + dead):
+            where[m] = (g, j)
+    return where
+
+
+def plan_gpu(L, lib, rs, p, lost, chunk, world, rank):
+    where = placement(p, lost, world)
+    nm = world * p
+    host = (c_int * nm)(*[where[m][0] for m in range(nm)])
+    slot = (c_int * nm)(*[where[m][1] for m in range(nm)])
+    W = int(lib.redset_hip_shard_slice_bytes(chunk, world))
+    base = 1 << 40  # addresses only: nothing is executed
+    lay = L.ShardLayout(world, host, slot, p, chunk, W, base, base + (1 << 38), base + (2 << 38), base + (3 << 38))
+    tr = L.Transport(world, rank, ctypes.cast(L.EXCHANGE_FN(lambda *a: 0), c_void_p), None)
+    cfn = L.COMPUTE_FN(lambda *a: 0)
+    comp = L.Compute(ctypes.cast(cfn, c_void_p), None)
+    out = c_void_p()
+    arr = (c_int * len(lost))(*lost)
+    if lib.redset_hip_rs_sharded_plan(rs, L.PLAN_RS_REBUILD, len(lost), arr, ctypes.byref(lay), ctypes.byref(tr),
+                                      ctypes.byref(comp), ctypes.byref(out)) != 0:
+        raise RuntimeError(lib.redset_hip_last_error().decode())
+    info = L.ShardedInfo()
+    lib.redset_hip_sharded_get_info(out, ctypes.byref(info))
+    lib.redset_hip_sharded_destroy(out)
+    return info.as_dict()
+
+
+def model(p, e, lost, chunk, world):
+    from redset_amd import _lib as L
+
+    lib = L.load()
+    rs = c_void_p()
+    lib.redset_hip_rs_create(p, e, ctypes.byref(rs))
+    rows = [plan_gpu(L, lib, rs, p, lost, chunk, world, g) for g in range(world)]
+    lib.redset_hip_rs_destroy(rs)
+    sent = max(r["gather_bytes_sent"] + r["return_bytes_sent"] for r in rows)
+    recv = max(r["gather_bytes_recv"] + r["return_bytes_recv"] for r in rows)
+    comp = max(r["compute_bytes"] for r in rows)
+    t_hbm = comp / (GF_MAC_REBUILD_GBPS * 1e9)
+    t_xgmi = max(sent, recv) / ((world - 1) * XGMI_LINK_GBPS * 1e9) if world > 1 else 0.0
+    step = max(t_hbm, t_xgmi)
+    alg = world * p * (p - e + len(lost)) * chunk
+    return {
+        "n_gpus": world,
+        "workload": f"{world} sets of RS({p - e}+{e}), chunk {chunk >> 20} MiB, rebuild {lost}, members round-robin",
+        "per_gpu_max": {"bytes_sent": sent, "bytes_recv": recv, "compute_bytes": comp,
+                        "messages_sent": max(r["gather_messages"] + r["return_messages"] for r in rows)},
+        "seconds": {"hbm": round(t_hbm, 6), "xgmi": round(t_xgmi, 6)},
+        "bound": "xgmi" if t_xgmi > t_hbm else "hbm",
+        "model_ms_per_step": round(step * 1e3, 4),
+        "model_value_GBps": round(alg / step / 1e9, 1),
+        "model_frac_of_hbm": round(alg / step / 1e9 / (world * 8000.0), 4),
+        "ceilings": {"xgmi_GBps_per_link": XGMI_LINK_GBPS, "gf_mac_rebuild_GBps": GF_MAC_REBUILD_GBPS},
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--chunk-mib", type=int, default=64)
+    ap.add_argument("--ranks", type=int, default=11)
+    ap.add_argument("--encoding", type=int, default=3)
+    ap.add_argument("--lost", default="1,2")
+    a = ap.parse_args()
+    lost = sorted(int(x) for x in a.lost.split(","))
+    for n in (1, 2, 4, 8):
+        print(json.dumps(model(a.ranks, a.encoding, lost, a.chunk_mib << 20, n)))
+
+
+if __name__ == "__main__":
+    main()

@@ -434,7 +434,15 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     runner.encode()
     snap = runner.lost_snapshot()
     runner.erase()
-    s_elapsed = timed(lambda i: runner.rebuild(), args.steps, args.warmup, dist_on, before=runner.reset_timing)
+    # the leg starts after a pause in GPU work (planning, the snapshot): its
+    # first ~25 steps run ~4% slow however they are split (the same loop
+    # right after runs at full rate, profiles/r05s22_sequence.json), so over
+    # RCCL it warms up for at least 25 steps whatever --warmup says (gloo
+    # rehearsals take seconds per step and keep --warmup)
+    warm = args.warmup
+    if args.warmup > 0 and dev == "cuda":
+        warm = max(args.warmup, SHARDED_MIN_WARMUP)
+    s_elapsed = timed(lambda i: runner.rebuild(), args.steps, warm, dist_on, before=runner.reset_timing)
     s_step = s_elapsed / args.steps
     torch.cuda.synchronize()
     hangs = redset_amd.hang_faults()
@@ -456,10 +464,10 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     # with every GPU's slices already in place, and the RCCL exchange (gather
     # + return) timed separately -- each K steps bracketed like the step,
     # max over ranks
-    d_step = timed(lambda i: runner.run_phases("rebuild", [L_PHASE_COMPUTE]), args.steps, args.warmup,
+    d_step = timed(lambda i: runner.run_phases("rebuild", [L_PHASE_COMPUTE]), args.steps, warm,
                    dist_on) / args.steps
     x_step = timed(lambda i: runner.run_phases("rebuild", [L_PHASE_GATHER, L_PHASE_RETURN]), args.steps,
-                   args.warmup, dist_on) / args.steps
+                   min(warm, args.warmup), dist_on) / args.steps
     decode_value = world * runner.algorithmic_bytes("rebuild") / d_step / 1e9
     # The step's roofline is the fabric, not HBM: every GPU sends its
     # share of the decode inputs' slices to every other GPU and gets the
@@ -563,6 +571,7 @@ def emit(result, rank):
 
 
 WATCHDOG_EXIT = 3
+SHARDED_MIN_WARMUP = 25
 
 
 def sharded_expired(result, rank, limit):

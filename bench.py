@@ -537,7 +537,57 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     # group does (every rank is past the same collectives here)
     torch.cuda.synchronize()
     runner.close()
+    if dist_on:
+        out["one_set"] = one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak)
+    else:
+        out["one_set"] = "at N = 1 the leg itself: one set on one GPU"
     return out
+
+
+def one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak):
+    """BASELINE.md's C4 word for word: ONE RS(8+3) set (configs[2]'s data)
+    column-sharded over the N GPUs -- strong scaling, member r on GPU r mod N,
+    every GPU rebuilding its 1/N column slice of every stripe. The same three
+    loops as the leg (the step, the decode on slices in place, the exchange
+    alone), K steps each, bracketed and max over ranks; bit-exact checked."""
+    import torch
+    import torch.distributed as dist
+
+    import redset_amd
+    from redset_amd import dist as rdist
+    from redset_amd._lib import PHASE_COMPUTE, PHASE_GATHER, PHASE_RETURN
+
+    runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, sets=1)
+    runner.timing = False
+    runner.encode()
+    snap = runner.lost_snapshot()
+    runner.erase()
+    dist_on = world > 1
+    step = timed(lambda i: runner.rebuild(), args.steps, warm, dist_on) / args.steps
+    torch.cuda.synchronize()
+    ok = reduce(1 if runner.matches(snap) and redset_amd.hang_faults() == 0 else 0, dist.ReduceOp.MIN, torch.int32)
+    d_step = timed(lambda i: runner.run_phases("rebuild", [PHASE_COMPUTE]), args.steps, warm, dist_on) / args.steps
+    x_step = timed(lambda i: runner.run_phases("rebuild", [PHASE_GATHER, PHASE_RETURN]), args.steps,
+                   min(warm, args.warmup), dist_on) / args.steps
+    total = runner.total_algorithmic_bytes("rebuild")
+    sent_mean = reduce(float(runner.exchanged_bytes("rebuild")), dist.ReduceOp.SUM, torch.float64) / world
+    torch.cuda.synchronize()
+    runner.close()
+    peak = world * HBM_PEAK_GBPS
+    return {
+        "workload": (f"one set of p={p} (RS({p - e}+{e}), chunk {chunk / MIB:g} MiB) over {world} GPUs, member r on "
+                     f"GPU r mod {world}; rebuild of {lost} (BASELINE.md C4, strong scaling)"),
+        "value": round(total / step / 1e9, 2),
+        "frac_of_hbm": round(total / step / 1e9 / peak, 6),
+        "ms_per_step": round(step * 1e3, 4),
+        "bit_exact": bool(ok),
+        "decode": {"value": round(total / d_step / 1e9, 2), "frac_of_hbm": round(total / d_step / 1e9 / peak, 6),
+                   "ms_per_step": round(d_step * 1e3, 4)},
+        "exchange_only": {"ms_per_step": round(x_step * 1e3, 4),
+                          "bytes_sent_per_gpu": int(sent_mean),
+                          "send_GBps_per_gpu": round(sent_mean / x_step / 1e9, 2) if sent_mean else None,
+                          "frac_of_xgmi": round(sent_mean / x_step / 1e9 / link_peak, 4) if sent_mean else None},
+    }
 
 
 _PRINT_LOCK = threading.Lock()

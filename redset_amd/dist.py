@@ -169,13 +169,16 @@ class CallbackCompute:
 
 
 class ShardedSetRunner:
-    """Encode + rebuild of `world` sets column-sharded over `world` ranks."""
+    """Encode + rebuild of `sets` sets (default `world`: weak scaling, one
+    set's worth of work per GPU) column-sharded over `world` ranks; sets = 1
+    spreads one set over all of them (strong scaling, BASELINE.md's C4)."""
 
     def __init__(self, p: int, e: int, chunk: int, lost: Sequence[int], world: int, rank: int,
                  device=None, backend=None, seed: int = 1234, fill: bool = True, transport: Optional[str] = None,
-                 parity_gap: Optional[int] = 0):
+                 parity_gap: Optional[int] = 0, sets: Optional[int] = None):
         self.p, self.e, self.d = p, e, p - e
         self.chunk, self.world, self.rank = chunk, world, rank
+        self.nsets = world if sets is None else sets
         self.lost = sorted(lost)
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         L = _lib.load()
@@ -191,7 +194,8 @@ class ShardedSetRunner:
         self.timing = self.device.type == "cuda"
         self.phased = False
         self._events = []
-        d, W, mh = self.d, self.W, p  # every GPU hosts p members
+        # members per GPU: p when there are `world` sets
+        d, W, mh = self.d, self.W, -(-self.nsets * p // world)
         u8 = dict(dtype=torch.uint8, device=self.device)
         if parity_gap is None:
             self.D_host = torch.zeros(world, mh, d, W, **u8)
@@ -222,10 +226,10 @@ class ShardedSetRunner:
         self._compute = CallbackCompute(backend, p, self._bufs) if backend is not None else None
         self._codec_h = c_void_p()
         _lib.check(L.redset_hip_rs_create(p, e, ctypes.byref(self._codec_h)), "rs_create")
-        nm = world * p
+        nm = self.nsets * p
         self._host_arr = (c_int * nm)(*[self._where[m][0] for m in range(nm)])
         self._slot_arr = (c_int * nm)(*[self._where[m][1] for m in range(nm)])
-        self._layout = _lib.ShardLayout(world, self._host_arr, self._slot_arr, mh, chunk, W,
+        self._layout = _lib.ShardLayout(self.nsets, self._host_arr, self._slot_arr, mh, chunk, W,
                                         self.D_host.data_ptr(), self.P_host.data_ptr(),
                                         self.D_gath.data_ptr(), self.P_gath.data_ptr())
         self._plans = {"encode": self._plan(_lib.PLAN_RS_ENCODE, [])}
@@ -266,7 +270,7 @@ class ShardedSetRunner:
         self.n_alive = []
         self._hosted = []
         for g in range(self.world):
-            mine = [m for m in range(self.world * self.p) if m % self.world == g]
+            mine = [m for m in range(self.nsets * self.p) if m % self.world == g]
             alive = [m for m in mine if (m % self.p) not in self.lost]
             dead = [m for m in mine if (m % self.p) in self.lost]
             for j, m in enumerate(alive + dead):
@@ -323,7 +327,7 @@ class ShardedSetRunner:
 
     def erase(self) -> None:
         """Model the loss of the lost members' files on their hosts."""
-        for k in range(self.world):
+        for k in range(self.nsets):
             for r in self.lost:
                 h, j = self.host_of(k, r)
                 if h == self.rank:
@@ -342,7 +346,7 @@ class ShardedSetRunner:
     def lost_snapshot(self) -> List[Tuple[int, torch.Tensor, torch.Tensor]]:
         """Copies of this GPU's hosted slabs of the members `erase` destroys."""
         snap = []
-        for k in range(self.world):
+        for k in range(self.nsets):
             for r in self.lost:
                 h, j = self.host_of(k, r)
                 if h == self.rank:
@@ -366,13 +370,18 @@ class ShardedSetRunner:
 
     # ---- accounting ------------------------------------------------------
     def algorithmic_bytes(self, op: str = "step") -> int:
-        """Per-GPU algorithmic bytes (one set's worth, p stripes): encode
+        """One set's algorithmic bytes (p stripes; per GPU when there are
+        `world` sets): encode
         (d+e)*C per stripe, rebuild (d+m)*C per stripe (SURVEY.md §8d);
         "step" = both."""
         p, d, e, m, C = self.p, self.d, self.e, len(self.lost), self.chunk
         enc = p * (d + e) * C
         reb = p * (d + m) * C if m else 0
         return {"encode": enc, "rebuild": reb, "step": enc + reb}[op]
+
+    def total_algorithmic_bytes(self, op: str = "step") -> int:
+        """All GPUs' algorithmic bytes per operation: every set's."""
+        return self.nsets * self.algorithmic_bytes(op)
 
     def exchanged_bytes(self, op: str = "step") -> int:
         """Bytes this GPU sends over the fabric per operation (C planner's count)."""
@@ -418,7 +427,7 @@ class ShardedSetRunner:
                 msgs[o] = {"gather_messages": i["gather_messages"], "return_messages": i["return_messages"],
                            "gather_msg_bytes": [i["gather_msg_min"], i["gather_msg_max"]],
                            "return_msg_bytes": [i["return_msg_min"], i["return_msg_max"]],
-                           "exchanges": 2 * self.world}
+                           "exchanges": 2 * self.nsets}
         out = {
             "exchange": {
                 "bytes_sent_per_gpu_per_step": self.exchanged_bytes(op),

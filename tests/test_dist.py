@@ -51,7 +51,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, p, e, chunk, lost, outdir):
+def _worker(rank, world, port, p, e, chunk, lost, outdir, sets=None):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -62,7 +62,7 @@ def _worker(rank, world, port, p, e, chunk, lost, outdir):
     from redset_amd.dist import ShardedSetRunner
 
     runner = ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, device="cpu",
-                              backend=OracleBackend(p, e), seed=99, transport="torch")
+                              backend=OracleBackend(p, e), seed=99, transport="torch", sets=sets)
     if rank == 0:
         import json
 
@@ -100,13 +100,17 @@ def _assemble(host_arrays, where, world, p, chunk, W, k, r):
     return np.concatenate(cells)
 
 
-@pytest.mark.parametrize("world,p,e,chunk,lost", [(2, 4, 2, 3000, [1]), (2, 11, 3, 4096, [1, 2]), (4, 11, 3, 2048, [1, 2]),
-                                                   (8, 11, 3, 4096, [1, 2]),  # the driver's 8-GPU shape
-                                                   (3, 5, 2, 1000, [0, 4])])
-def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost):
+@pytest.mark.parametrize("world,p,e,chunk,lost,sets", [
+    (2, 4, 2, 3000, [1], None), (2, 11, 3, 4096, [1, 2], None), (4, 11, 3, 2048, [1, 2], None),
+    (8, 11, 3, 4096, [1, 2], None),  # the driver's 8-GPU shape
+    (3, 5, 2, 1000, [0, 4], None),
+    # one set spread over every GPU (strong scaling, BASELINE.md's C4)
+    (2, 11, 3, 4096, [1, 2], 1), (3, 5, 2, 1000, [0, 4], 1), (8, 11, 3, 4096, [1, 2], 1)])
+def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost, sets):
     port = _free_port()
+    nsets = world if sets is None else sets
     with tempfile.TemporaryDirectory() as td:
-        mp.spawn(_worker, args=(world, port, p, e, chunk, lost, td), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, port, p, e, chunk, lost, td, sets), nprocs=world, join=True)
         load = lambda name: [np.load(os.path.join(td, f"{name}_{g}.npy")) for g in range(world)]
         data, par, data2, par2 = load("data"), load("par"), load("data2"), load("par2")
         W = data[0].shape[-1]
@@ -120,7 +124,7 @@ def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost):
 
         need_d, need_p = rebuild_inputs(p, e, lost)
         cells_in = sum(int(need_d[r].sum() + need_p[r].sum()) for r in range(p))
-        want_sent = world * (world - 1) * W * (cells_in + len(lost) * p)
+        want_sent = nsets * (world - 1) * W * (cells_in + len(lost) * p)
         sent = 0
         for g in range(world):
             with open(os.path.join(td, f"sent_{g}.json")) as f:
@@ -128,7 +132,7 @@ def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost):
         assert sent == want_sent
         assert cells_in == p * (p - e)
         st = oracle.OracleRS(p, e)
-        for k in range(world):
+        for k in range(nsets):
             lofi = [_assemble(data, where, world, p, chunk, W, k, r) for r in range(p)]
             want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
             st.encode_set(lofi, want, chunk)

@@ -52,6 +52,10 @@ def _check_sharded(sh, world):
         assert msgs["gather_messages"] > 0 and msgs["return_messages"] > 0, msgs
         assert sh["exchange"]["bytes_sent_per_gpu_per_step"] > 0
         assert sh["exchange_only"]["send_GBps_per_gpu"] > 0, sh["exchange_only"]
+        # BASELINE.md C4 word for word: one set over every GPU (strong scaling)
+        one = sh["one_set"]
+        assert one["bit_exact"] is True and one["value"] > 0 and one["decode"]["value"] > 0, one
+        assert one["exchange_only"]["bytes_sent_per_gpu"] > 0, one
     else:
         assert msgs["gather_messages"] == 0 and msgs["return_messages"] == 0, msgs
         assert sh["roofline"]["bound"] == "hbm" and sh["exchange"]["bytes_sent_per_gpu_per_step"] == 0

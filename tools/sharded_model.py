@@ -11,14 +11,15 @@ bytes of its compute, and prices them:
   xgmi   max(sent, recv) / ((N - 1) x 153 GB/s): an all-to-all over the
          fully connected mesh, one link per GPU pair
   hbm    compute bytes / the measured gf_mac rebuild rate (6.3 TB/s,
-         profiles/r05s13_bench_kernel_stats.csv)
+         profiles/r05s24_bench_kernel_stats.csv)
 
 The leg pipelines its sets (set k + 1's gather under set k's gf_mac), so a
 step costs about the larger of the two; `model_value` is then N sets'
 algorithmic rebuild bytes over that. SCALE_rNN's sharded.value at each N is
-to be read against it.
+to be read against it. --one-set: one set spread over the N GPUs instead
+(the leg's `one_set`, BASELINE.md's C4 word for word).
 
-usage: python tools/sharded_model.py [--chunk-mib 64] [--ranks 11] [--encoding 3] [--lost 1,2]
+usage: python tools/sharded_model.py [--chunk-mib 64] [--ranks 11] [--encoding 3] [--lost 1,2] [--one-set]
 """
 import argparse
 import ctypes
@@ -34,11 +35,11 @@ XGMI_LINK_GBPS = 153.0
 GF_MAC_REBUILD_GBPS = 6300.0
 
 
-def placement(p, lost, world):
+def placement(p, lost, world, nsets):
     """dist.py ShardedSetRunner._place: (host, slot) of every member"""
     where = {}
     for g in range(world):
-        mine = [m for m in range(world * p) if m % world == g]
+        mine = [m for m in range(nsets * p) if m % world == g]
         alive = [m for m in mine if (m % p) not in lost]
         dead = [m for m in mine if (m % p) in lost]
         for j, m in enumerate(alive + dead):
@@ -46,14 +47,15 @@ def placement(p, lost, world):
     return where
 
 
-def plan_gpu(L, lib, rs, p, lost, chunk, world, rank):
-    where = placement(p, lost, world)
-    nm = world * p
+def plan_gpu(L, lib, rs, p, lost, chunk, world, rank, nsets):
+    where = placement(p, lost, world, nsets)
+    nm = nsets * p
     host = (c_int * nm)(*[where[m][0] for m in range(nm)])
     slot = (c_int * nm)(*[where[m][1] for m in range(nm)])
     W = int(lib.redset_hip_shard_slice_bytes(chunk, world))
     base = 1 << 40  # addresses only: nothing is executed
-    lay = L.ShardLayout(world, host, slot, p, chunk, W, base, base + (1 << 38), base + (2 << 38), base + (3 << 38))
+    lay = L.ShardLayout(nsets, host, slot, -(-nsets * p // world), chunk, W, base, base + (1 << 38),
+                        base + (2 << 38), base + (3 << 38))
     tr = L.Transport(world, rank, ctypes.cast(L.EXCHANGE_FN(lambda *a: 0), c_void_p), None)
     cfn = L.COMPUTE_FN(lambda *a: 0)
     comp = L.Compute(ctypes.cast(cfn, c_void_p), None)
@@ -68,13 +70,14 @@ def plan_gpu(L, lib, rs, p, lost, chunk, world, rank):
     return info.as_dict()
 
 
-def model(p, e, lost, chunk, world):
+def model(p, e, lost, chunk, world, one_set=False):
     from redset_amd import _lib as L
 
     lib = L.load()
     rs = c_void_p()
     lib.redset_hip_rs_create(p, e, ctypes.byref(rs))
-    rows = [plan_gpu(L, lib, rs, p, lost, chunk, world, g) for g in range(world)]
+    nsets = 1 if one_set else world
+    rows = [plan_gpu(L, lib, rs, p, lost, chunk, world, g, nsets) for g in range(world)]
     lib.redset_hip_rs_destroy(rs)
     sent = max(r["gather_bytes_sent"] + r["return_bytes_sent"] for r in rows)
     recv = max(r["gather_bytes_recv"] + r["return_bytes_recv"] for r in rows)
@@ -82,10 +85,11 @@ def model(p, e, lost, chunk, world):
     t_hbm = comp / (GF_MAC_REBUILD_GBPS * 1e9)
     t_xgmi = max(sent, recv) / ((world - 1) * XGMI_LINK_GBPS * 1e9) if world > 1 else 0.0
     step = max(t_hbm, t_xgmi)
-    alg = world * p * (p - e + len(lost)) * chunk
+    alg = nsets * p * (p - e + len(lost)) * chunk
     return {
         "n_gpus": world,
-        "workload": f"{world} sets of RS({p - e}+{e}), chunk {chunk >> 20} MiB, rebuild {lost}, members round-robin",
+        "workload": (f"{nsets} set(s) of RS({p - e}+{e}) over {world} GPUs, chunk {chunk >> 20} MiB, rebuild {lost}, "
+                     "members round-robin"),
         "per_gpu_max": {"bytes_sent": sent, "bytes_recv": recv, "compute_bytes": comp,
                         "messages_sent": max(r["gather_messages"] + r["return_messages"] for r in rows)},
         "seconds": {"hbm": round(t_hbm, 6), "xgmi": round(t_xgmi, 6)},
@@ -103,10 +107,11 @@ def main():
     ap.add_argument("--ranks", type=int, default=11)
     ap.add_argument("--encoding", type=int, default=3)
     ap.add_argument("--lost", default="1,2")
+    ap.add_argument("--one-set", action="store_true", help="one set over the N GPUs (the leg's one_set, C4)")
     a = ap.parse_args()
     lost = sorted(int(x) for x in a.lost.split(","))
     for n in (1, 2, 4, 8):
-        print(json.dumps(model(a.ranks, a.encoding, lost, a.chunk_mib << 20, n)))
+        print(json.dumps(model(a.ranks, a.encoding, lost, a.chunk_mib << 20, n, a.one_set)))
 
 
 if __name__ == "__main__":

@@ -95,7 +95,8 @@ int redset_hip_rank_last_exchange(void);
 /* What the calling thread's last backend call moved and where it waited
  * (one member's view): bytes read from the logical file and the redundancy
  * file, sent and received over MPI (or, sharded, over the exchange's
- * transport), copied to and from the GPU, written; and the seconds its host
+ * transport), copied to and from the GPU (over host slabs, _SHARDED_HOST: the
+ * kernels' own reads and writes across PCIe), written; and the seconds its host
  * thread spent blocked, in disjoint classes whose sum is at most the call:
  *   read / write_seconds   file I/O
  *   mpi_seconds            MPI waits: the exchanges' Waitall (the MPI
@@ -111,9 +112,9 @@ int redset_hip_rank_last_exchange(void);
  *                          (and creating / destroying a _SHARDED_MPI
  *                          transport), scratch buffers and stream from the
  *                          cache or new, events, tearing the plans down
- * exchange_seconds is the host time inside redset_hip_sharded_execute (the
- * sharded calls' exchanges and kernels; it contains their mpi, gpu and stage
- * time and is not one of the classes). */
+ * exchange_seconds is the host time inside redset_hip_sharded_execute and
+ * its phases (the sharded calls' exchanges and kernels; it contains their
+ * mpi, gpu and stage time and is not one of the classes). */
 typedef struct {
   double seconds;
   double read_seconds, mpi_seconds, gpu_seconds, write_seconds;

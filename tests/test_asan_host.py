@@ -9,7 +9,12 @@ are the regular build's -- and these tests drive them:
   exchanges and teardown must be free of invalid accesses and leaks;
 * the offline tool's header reader (header_tree.c) on intact, truncated and
   bit-flipped redundancy-file headers: it may refuse a header, never read
-  out of bounds.
+  out of bounds;
+* the drop-in slot's per-rank backends (rank_mpi.c, instrumented, with the
+  HIP stand-in tests/mpi/hipstub.c preloaded as in test_mpi_hoststub.py):
+  the host ring, the sharded plan over device buffers and over host slabs,
+  two calls per process (the second on the cached scratch and slot context),
+  encode and rebuild checked against the oracle, leak checking on.
 """
 import os
 import shutil
@@ -122,3 +127,23 @@ def test_header_set_discovery_asan(asan_build, tmp_path):
     res = subprocess.run([tool, "headers", *reds], capture_output=True, text=True, errors="replace", timeout=60, env=ENV)
     assert _clean(res), res.stderr[-4000:]
     assert res.returncode == 1 and "3 members missing" in res.stderr, res.stderr[-2000:]
+
+
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="needs MPICH's mpirun")
+@pytest.mark.parametrize("exchange", ["host", "sharded-mpi", "sharded-host"])
+@pytest.mark.parametrize("scheme,p,e,lost", [("rs", 6, 2, [1, 4]), ("rs", 5, 3, [0, 2, 4]), ("xor", 4, 1, [2])])
+def test_slot_backends_asan(asan_build, oracle, tmp_path, exchange, scheme, p, e, lost):
+    """rank_mpi.c's host code (the instrumented product build: tests/asan's
+    libredset_hip_mpi.so, loaded through rank_test's RUNPATH) under ASan +
+    LeakSanitizer, for every exchange of the slot."""
+    import test_mpi_hoststub as hs
+
+    if not os.path.exists(hs.MPIRUN):
+        pytest.skip("needs MPICH")
+    subprocess.run(["make", "-s", "-C", hs.MPI_DIR], check=True, capture_output=True)
+    env = {"_DRIVER": os.path.join(asan_build, "rank_test"), "RANK_TEST_EXCHANGE": exchange, "RANK_TEST_REPEAT": "2",
+           "ASAN_OPTIONS": "verify_asan_link_order=0:detect_leaks=1:halt_on_error=1:exitcode=86",
+           "LSAN_OPTIONS": "suppressions=" + os.path.join(ASAN_DIR, "lsan.supp")}
+    enc, reb, _ = hs._round_trip(oracle, str(tmp_path), scheme, p, e, lost, 16384, 300 + p, 120_000, env=env)
+    for res in (enc, reb):
+        assert f"exchange {exchange}" in res.stdout, res.stdout

@@ -46,7 +46,7 @@ def _run(np_, args, env=None, timeout=120):
     drv = env.pop("_DRIVER", RANK_TEST)
     cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", "-env", "LD_PRELOAD", STUB, drv] + [str(a) for a in args]
     res = run_group(cmd, timeout, env=env)
-    assert "AddressSanitizer" not in res.stderr, res.stderr[-4000:]
+    assert "AddressSanitizer" not in res.stderr and "LeakSanitizer" not in res.stderr, res.stderr[-4000:]
     return res
 
 

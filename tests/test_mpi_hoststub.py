@@ -297,3 +297,31 @@ def test_sharded_slot_without_the_cache_plans_every_call(stub, oracle, tmp_path,
     enc, reb, _ = _round_trip(oracle, str(tmp_path), "rs", 5, 2, [1, 3], 32768, 77, 200_000, env=env)
     for res in (enc, reb):
         assert _stats(res.stdout, "warm")["plan_seconds"][0] > 0, res.stdout
+
+
+@pytest.mark.parametrize("scheme,p,e,want", [("rs", 6, 2, "sharded-host"), ("rs", 5, 1, "host"), ("xor", 4, 1, "host"),
+                                             ("rs", 33, 2, "host")])
+def test_auto_encode_exchange(stub, oracle, tmp_path, scheme, p, e, want):
+    """AUTO's encode (rank_mpi.c choose_exchange): the host slabs for RS with
+    e >= 2 up to p = 32 (fewer bytes than the ring), the host ring for XOR,
+    e = 1 (the same bytes) and wider sets (a window's messages shrink as
+    1/p); either way bit-exact against the oracle."""
+    env = {k: v for k, v in os.environ.items() if k != "RANK_TEST_EXCHANGE"}
+    env["_DRIVER"] = RANK_TEST
+    tmp = str(tmp_path)
+    d = p - e
+    rng = np.random.default_rng(p)
+    files, chunk = _setup(tmp, p, d, rng, 3000)
+    reds = [os.path.join(tmp, f"r{r}.{scheme}.redset") for r in range(p)]
+    _manifests(tmp, files, chunk, [100] * p, reds)
+    res = _run(p, [scheme, "encode", e, tmp, 4096], env=env, timeout=240)
+    assert res.returncode == 0, res.stdout + res.stderr[-3000:]
+    assert f"encode exchange {want}" in res.stdout, res.stdout
+    lofi = [_logical(fl, d * chunk) for fl in files]
+    par = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
+    if scheme == "rs":
+        oracle.OracleRS(p, e).encode_set(lofi, par, chunk)
+    else:
+        oracle.xor_encode_set(p, lofi, par, chunk)
+    for r in range(p):
+        assert np.array_equal(np.fromfile(reds[r], dtype=np.uint8)[100:], par[r]), r

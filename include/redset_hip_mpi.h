@@ -63,7 +63,7 @@ int redset_hip_xor_decode_rank(MPI_Comm comm, int root, const redset_hip_io* lof
  * the rebuilt slices to the lost members (replacing the decode ring and
  * gather, src/redset_reedsolomon.c:646-733, and the XOR reduce to the root,
  * src/redset_xor.c:466-524); decodes elsewhere take the host-MPI paths
- * above. An RS ENCODE with e >= 2 and p <= 32 runs as the sharded plan over
+ * above. An RS ENCODE with d, e >= 2 and p <= 32 runs as the sharded plan over
  * host slabs (_SHARDED_HOST below: it sends (d + e)(p - 1)/p cells per member
  * where the reference's ring sends d*e, RS(8+3) 10 against 24); XOR and e = 1
  * encodes, where the two send the same, and wider sets, whose windows would

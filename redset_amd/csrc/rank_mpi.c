@@ -1331,15 +1331,15 @@ static int rccl_create(MPI_Comm comm, int p, int r, comm_exchange* X) {
  *   AUTO_DECODE       RCCL when the members each own a GPU of one node, else
  *                     the host path
  *   AUTO_ENCODE_SLABS the sharded plan over host slabs (_SHARDED_HOST): an RS
- *                     encode with e >= 2 and p <= AUTO_SLABS_MAX_P, where it
+ *                     encode with d, e >= 2 and p <= AUTO_SLABS_MAX_P, where it
  *                     sends (d + e)(p - 1)/p cells per member against the
  *                     ring's d*e (RS(8+3): 10 against 24) and measured faster
  *                     on one box too (profiles/r05s12_rank_roofline.jsonl,
  *                     r05s26_rank_roofline_rs10p4.jsonl: p = 11, 14). Past
  *                     that a window's messages shrink as 1/p (its slices as
  *                     1/p^2), where the ring keeps whole slices
- *   AUTO_ENCODE_HOST  the host ring: XOR and RS with e = 1 encodes, where the
- *                     two send the same bytes
+ *   AUTO_ENCODE_HOST  the host ring: XOR encodes and RS ones with e = 1 or
+ *                     d = 1, where the two send the same bytes, and wider sets
  * AUTO never sends an encode over RCCL: north_star asks for RCCL "only for
  * the multi-rank rebuild case", and an encode over RCCL has not yet run on a
  * node with a GPU per member; forcing _SHARDED_RCCL still does. */
@@ -1886,8 +1886,9 @@ static int encode_rank(const redset_hip_rs* rs, MPI_Comm comm, const redset_hip_
   if (B > (size_t) INT_MAX) return fail("buf_size %zu exceeds an MPI count", B); /* same on every rank */
   int mode;
   comm_exchange* X = NULL;
-  if (choose_exchange(comm, p, r, rs && e >= 2 && p <= AUTO_SLABS_MAX_P ? AUTO_ENCODE_SLABS : AUTO_ENCODE_HOST, &mode,
-                      &X))
+  /* fewer bytes than the ring needs d >= 2 and e >= 2: (d + e)(p - 1)/p < d*e */
+  const int slabs = rs && e >= 2 && p - e >= 2 && p <= AUTO_SLABS_MAX_P;
+  if (choose_exchange(comm, p, r, slabs ? AUTO_ENCODE_SLABS : AUTO_ENCODE_HOST, &mode, &X))
     return REDSET_FAILURE;
   g_last_exchange = mode;
   int rc;

@@ -62,15 +62,15 @@ def _exchange_env(exchange):
     return {"RANK_TEST_EXCHANGE": exchange}
 
 
-def _auto_exchange(op, scheme, e):
+def _auto_exchange(op, scheme, e, p):
     """what AUTO picks on the test box (its members share one GPU): the host
     path, but an RS encode with e >= 2 over host slabs (rank_mpi.c
     choose_exchange, AUTO_ENCODE_SLABS)"""
-    return "sharded-host" if op == "encode" and scheme == "rs" and e >= 2 else "host"
+    return "sharded-host" if op == "encode" and scheme == "rs" and e >= 2 and p - e >= 2 and p <= 32 else "host"
 
 
-def _check_exchange(res, exchange, op="rebuild", scheme="rs", e=2):
-    used = _auto_exchange(op, scheme, e) if exchange == "auto" else exchange.replace("-windows", "")
+def _check_exchange(res, exchange, op="rebuild", scheme="rs", e=2, p=6):
+    used = _auto_exchange(op, scheme, e, p) if exchange == "auto" else exchange.replace("-windows", "")
     assert f"{op} exchange {used}" in res.stdout, res.stdout
 
 
@@ -122,7 +122,7 @@ def test_mpi_rank_backends(oracle, tmp_path, scheme, p, e, lost, buf, exchange):
 
     res = _mpirun(p, [scheme, "encode", e, tmp, buf], env=_exchange_env(exchange))
     assert res.returncode == 0, res.stdout + res.stderr
-    _check_exchange(res, exchange, "encode", scheme, e)
+    _check_exchange(res, exchange, "encode", scheme, e, p)
     lofi = [_logical(fl, d * chunk) for fl in files]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     if scheme == "rs":
@@ -274,7 +274,7 @@ def test_mpi_config0_xor_4_ranks_16MiB(oracle, tmp_path, exchange):
     _manifests(tmp, files, chunk, header, reds)
     res = _mpirun(p, ["xor", "encode", e, tmp, 1 << 20], env=_exchange_env(exchange))
     assert res.returncode == 0, res.stdout + res.stderr
-    _check_exchange(res, exchange, "encode", "xor", e)
+    _check_exchange(res, exchange, "encode", "xor", e, p)
     lofi = [_logical(fl, (p - 1) * chunk) for fl in files]
     want = [np.zeros(chunk, np.uint8) for _ in range(p)]
     oracle.xor_encode_set(p, lofi, want, chunk)
@@ -335,7 +335,7 @@ def test_mpi_rank_backends_repeated_calls(oracle, tmp_path, scheme, p, e, lost, 
     cmd = [MPIRUN, "-np", str(p), "-host", "localhost", RANK_TEST, scheme, "encode", str(e), tmp, "32768"]
     res = run_group(cmd, 120, env=env)
     assert res.returncode == 0 and "call 3 of 3" in res.stdout, res.stdout + res.stderr
-    _check_exchange(res, exchange, "encode", scheme, e)
+    _check_exchange(res, exchange, "encode", scheme, e, p)
     lofi = [_logical(fl, d * chunk) for fl in files]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     if scheme == "rs":
@@ -384,7 +384,7 @@ def test_mpi_rank_backends_random(oracle, tmp_path, seed):
     exchange = EXCHANGES[seed % len(EXCHANGES)]
     res = _mpirun(p, [scheme, "encode", e, tmp, buf], timeout=120, env=_exchange_env(exchange))
     assert res.returncode == 0, (scheme, p, e, buf, exchange, res.stdout + res.stderr)
-    _check_exchange(res, exchange, "encode", scheme, e)
+    _check_exchange(res, exchange, "encode", scheme, e, p)
     lofi = [_logical(fl, d * chunk) for fl in files]
     want = [np.zeros(e * chunk, np.uint8) for _ in range(p)]
     if scheme == "rs":
@@ -573,7 +573,7 @@ def test_mpi_auto_rebuild_takes_rccl_with_a_gpu_per_member(oracle, tmp_path, sch
     env = {"RANK_TEST_DEVICE_PER_RANK": "1"}
     res = _mpirun(p, [scheme, "encode", e, tmp, 1 << 20], env=env)
     assert res.returncode == 0, res.stdout + res.stderr
-    assert f"encode exchange {_auto_exchange('encode', scheme, e)}" in res.stdout, res.stdout
+    assert f"encode exchange {_auto_exchange('encode', scheme, e, p)}" in res.stdout, res.stdout
     for r in lost:
         for path, _ in files[r]:
             os.unlink(path)

@@ -300,12 +300,12 @@ def test_sharded_slot_without_the_cache_plans_every_call(stub, oracle, tmp_path,
 
 
 @pytest.mark.parametrize("scheme,p,e,want", [("rs", 6, 2, "sharded-host"), ("rs", 5, 1, "host"), ("xor", 4, 1, "host"),
-                                             ("rs", 33, 2, "host")])
+                                             ("rs", 3, 2, "host"), ("rs", 33, 2, "host")])
 def test_auto_encode_exchange(stub, oracle, tmp_path, scheme, p, e, want):
     """AUTO's encode (rank_mpi.c choose_exchange): the host slabs for RS with
-    e >= 2 up to p = 32 (fewer bytes than the ring), the host ring for XOR,
-    e = 1 (the same bytes) and wider sets (a window's messages shrink as
-    1/p); either way bit-exact against the oracle."""
+    d, e >= 2 up to p = 32 (fewer bytes than the ring), the host ring for XOR,
+    e = 1 or d = 1 (the same bytes) and wider sets (a window's messages shrink
+    as 1/p); either way bit-exact against the oracle."""
     env = {k: v for k, v in os.environ.items() if k != "RANK_TEST_EXCHANGE"}
     env["_DRIVER"] = RANK_TEST
     tmp = str(tmp_path)

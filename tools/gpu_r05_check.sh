@@ -1,8 +1,10 @@
 #!/bin/bash
-# Round-5 first GPU check: the new tests (bench self-launch, sharded leg at
-# N=1, hang-word contract in the twin and through the slot), then the whole
-# GPU suite, smoke and the default bench. Stops at the first step that
-# faults / aborts / times out (exit >= 2).
+# Round 5's one-call GPU session (r05s2 ... r05s28): the round's new tests
+# (bench self-launch, sharded leg at N=1, hang-word contract in the twin and
+# through the slot), the whole GPU suite (which reruns itself against the
+# test twin), smoke, the driver's bench command, a rocprofv3 kernel-stats run
+# and separate PMC FETCH_SIZE / WRITE_SIZE passes. Stops at the first step
+# that faults / aborts / times out (exit >= 2). usage: gpu_r05_check.sh <tag>
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
 OUT=gpurun_out/${1:-r05check}; mkdir -p "$OUT"

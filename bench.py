@@ -44,6 +44,7 @@ sys.path.insert(0, ROOT)
 
 # xGMI: per link and direction (7 links x ~153 GB/s per GPU)
 XGMI_LINK_GBPS = 153.0
+MODEL_GF_MAC_GBPS = 6300.0  # the whole-set rebuild's measured rate, for the sharded leg's model
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec peak (MI355X_MICROARCH.md)
 MIB = 1 << 20
 
@@ -453,6 +454,8 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     sent_mine = float(runner.exchanged_bytes("rebuild"))
     sent_mean = reduce(sent_mine, dist.ReduceOp.SUM, torch.float64) / world
     sent_max = reduce(sent_mine, dist.ReduceOp.MAX, torch.float64)
+    info = runner.info("rebuild")
+    recv_max = reduce(float(info["gather_bytes_recv"] + info["return_bytes_recv"]), dist.ReduceOp.MAX, torch.float64)
     # untimed diagnostic: the same rebuild with its three phases one after
     # another (no overlap across sets), timed apart by events on rank 0
     pipelined_event_ms = runner.phase_ms().get("rebuild_start->done")
@@ -507,6 +510,17 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
             "peak": HBM_PEAK_GBPS,
             "unit": "GB/s (algorithmic bytes / step time)",
             "frac": round(runner.algorithmic_bytes("rebuild") / s_step / 1e9 / HBM_PEAK_GBPS, 4),
+        },
+        # what the planner's bytes predict for this step (tools/sharded_model.py):
+        # the exchange at (N - 1) x 153 GB/s per GPU against the gf_mac at the
+        # measured whole-set rebuild rate; the step costs about the larger
+        "model": {
+            "xgmi_ms": round(max(sent_max, recv_max) / (link_peak * 1e9) * 1e3, 4) if dist_on else 0.0,
+            "hbm_ms": round(info["compute_bytes"] / (MODEL_GF_MAC_GBPS * 1e9) * 1e3, 4),
+            "value": round(world * runner.algorithmic_bytes("rebuild") / max(
+                max(sent_max, recv_max) / (link_peak * 1e9) if dist_on else 0.0,
+                info["compute_bytes"] / (MODEL_GF_MAC_GBPS * 1e9)) / 1e9, 1),
+            "note": f"{XGMI_LINK_GBPS:g} GB/s per xGMI link (platform figure), gf_mac {MODEL_GF_MAC_GBPS:g} GB/s",
         },
         # C4's decode alone, slices in place (all GPUs, max over ranks)
         "decode": {

@@ -349,6 +349,20 @@ int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, c
 int redset_hip_xor_sharded_plan(int ranks, int kind, int root, const redset_hip_shard_layout* layout,
                                 const redset_hip_transport* transport, const redset_hip_compute* compute,
                                 redset_hip_sharded** out);
+/* The same plans with only some processes computing: compute_on[g] != 0 for
+ * the K processes that take a column slice each (in rank order, slices
+ * 0 .. K - 1; slice_bytes >= ceil(chunk_size / K); NULL: all of them, as
+ * above). The others only send the cells they host and receive their
+ * members' outputs -- e.g. a rebuild whose lost members then receive just
+ * their own cells instead of also gathering a slice of every decode input.
+ * Every process must pass the same mask. */
+int redset_hip_rs_sharded_plan_on(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
+                                  const redset_hip_shard_layout* layout, const int* compute_on,
+                                  const redset_hip_transport* transport, const redset_hip_compute* compute,
+                                  redset_hip_sharded** out);
+int redset_hip_xor_sharded_plan_on(int ranks, int kind, int root, const redset_hip_shard_layout* layout,
+                                   const int* compute_on, const redset_hip_transport* transport,
+                                   const redset_hip_compute* compute, redset_hip_sharded** out);
 /* All three phases, ordered after the work already on `stream`; work
  * enqueued on `stream` afterwards sees the results. With the HIP plans as
  * compute (compute == NULL at plan time) the sets are pipelined: every set's

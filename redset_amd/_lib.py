@@ -61,6 +61,8 @@ EXPORTED_SYMBOLS = (
     "redset_hip_shard_slice_bytes",
     "redset_hip_rs_sharded_plan",
     "redset_hip_xor_sharded_plan",
+    "redset_hip_rs_sharded_plan_on",
+    "redset_hip_xor_sharded_plan_on",
     "redset_hip_sharded_execute",
     "redset_hip_sharded_execute_phase",
     "redset_hip_sharded_get_info",
@@ -226,6 +228,12 @@ _SIGNATURES = {
                 POINTER(c_void_p)]),
     "redset_hip_xor_sharded_plan": (
         c_int, [c_int, c_int, c_int, POINTER(ShardLayout), POINTER(Transport), POINTER(Compute), POINTER(c_void_p)]),
+    "redset_hip_rs_sharded_plan_on": (
+        c_int, [c_void_p, c_int, c_int, POINTER(c_int), POINTER(ShardLayout), POINTER(c_int), POINTER(Transport),
+                POINTER(Compute), POINTER(c_void_p)]),
+    "redset_hip_xor_sharded_plan_on": (
+        c_int, [c_int, c_int, c_int, POINTER(ShardLayout), POINTER(c_int), POINTER(Transport), POINTER(Compute),
+                POINTER(c_void_p)]),
     "redset_hip_sharded_execute": (c_int, [c_void_p, c_void_p]),
     "redset_hip_sharded_execute_phase": (c_int, [c_void_p, c_int, c_void_p]),
     "redset_hip_sharded_get_info": (c_int, [c_void_p, POINTER(ShardedInfo)]),

@@ -216,6 +216,8 @@ typedef struct {
   int p, e, d, mh, world, me, kind, missing;
   const int* lost;
   size_t W;
+  const int* sidx;            /* [world] the column slice a process computes, or -1 */
+  int me_s;                   /* mine */
 } pctx;
 
 /* addresses in this process's buffers (include/redset_hip.h layout) */
@@ -239,11 +241,12 @@ static int wanted(const pctx* C, int r, int pass, int x) {
   return 0;
 }
 
-/* set k's gather: slice g of every needed cell of every surviving member of
- * the set goes from its host to process g; data rows then parity rows,
- * members in slot order (both ends of a pair walk the same rows). My own
- * slice of the members I host stays where it is: the compute reads it in
- * the hosted slabs (plan_sets), so nothing is copied within the process */
+/* set k's gather: slice sidx[g] of every needed cell of every surviving
+ * member of the set goes from its host to each computing process g; data
+ * rows then parity rows, members in slot order (both ends of a pair walk the
+ * same rows). My own slice of the members I host stays where it is: the
+ * compute reads it in the hosted slabs (plan_sets), so nothing is copied
+ * within the process */
 static int plan_gather(const pctx* C, int k, exch* G) {
   const int me = C->me;
   int rc = 0;
@@ -251,15 +254,15 @@ static int plan_gather(const pctx* C, int k, exch* G) {
     if (g == me) continue;
     for (int pass = 0; pass < 2 && !rc; ++pass) {
       const int ncell = pass == 0 ? C->d : C->e;
-      for (int j = 0; j < C->mh && !rc; ++j) { /* what I send to g */
+      for (int j = 0; j < C->mh && !rc && C->sidx[g] >= 0; ++j) { /* what I send to g */
         const int m = C->by_slot[(size_t) me * C->mh + j];
         if (m < 0 || m / C->p != k) continue;
         for (int x = 0; x < ncell && !rc; ++x) {
           if (!wanted(C, m % C->p, pass, x)) continue;
-          rc = ex_send(G, g, pass == 0 ? hd(C, g, j, x) : hp(C, g, j, x), C->W);
+          rc = ex_send(G, g, pass == 0 ? hd(C, C->sidx[g], j, x) : hp(C, C->sidx[g], j, x), C->W);
         }
       }
-      for (int j = 0; j < C->mh && !rc; ++j) { /* my slice of g's members' needed cells */
+      for (int j = 0; j < C->mh && !rc && C->me_s >= 0; ++j) { /* my slice of g's members' needed cells */
         const int m = C->by_slot[(size_t) g * C->mh + j];
         if (m < 0 || m / C->p != k) continue;
         for (int x = 0; x < ncell && !rc; ++x)
@@ -271,8 +274,8 @@ static int plan_gather(const pctx* C, int k, exch* G) {
 }
 
 /* set k's return: the outputs (encode: every member's parity; rebuild: every
- * cell of the lost members) go from each process's gathered slots to the
- * member's host: data rows, then parity rows, members in set order. A
+ * cell of the lost members) go from each computing process's gathered slots
+ * to the member's host: data rows, then parity rows, members in set order. A
  * member I host got my slice in place (the compute wrote its hosted slab) */
 static int plan_return(const pctx* C, int k, exch* R) {
   int rc = 0;
@@ -285,20 +288,22 @@ static int plan_return(const pctx* C, int k, exch* R) {
       const int h = C->L->host[m], j = C->L->slot[m];
       const size_t len = (size_t) (pass == 0 ? C->d : C->e) * C->W;
       if (h != C->me) {
-        rc = ex_send(R, h, pass == 0 ? gd(C, h, j, 0) : gp(C, h, j, 0), len);
+        if (C->me_s >= 0) rc = ex_send(R, h, pass == 0 ? gd(C, h, j, 0) : gp(C, h, j, 0), len);
         continue;
       }
       for (int g = 0; g < C->world && !rc; ++g)
-        if (g != C->me) rc = ex_recv(R, g, pass == 0 ? hd(C, g, j, 0) : hp(C, g, j, 0), len);
+        if (g != C->me && C->sidx[g] >= 0)
+          rc = ex_recv(R, g, pass == 0 ? hd(C, C->sidx[g], j, 0) : hp(C, C->sidx[g], j, 0), len);
     }
   }
   return rc;
 }
 
-/* the plan of either scheme: rs (RS kinds) or NULL (XOR kinds, e = 1) */
+/* the plan of either scheme: rs (RS kinds) or NULL (XOR kinds, e = 1);
+ * compute: which processes compute a column slice (NULL: all) */
 static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missing, const int* rebuild_ranks,
-                     const redset_hip_shard_layout* L, const redset_hip_transport* tr, const redset_hip_compute* comp,
-                     redset_hip_sharded** out) {
+                     const redset_hip_shard_layout* L, const int* compute, const redset_hip_transport* tr,
+                     const redset_hip_compute* comp, redset_hip_sharded** out) {
   if (is_encode(kind)) missing = 0;
   if (!is_encode(kind)) {
     if (missing < 1 || missing > e) return sfail("cannot rebuild %d members with %d parity chunks", missing, e);
@@ -310,20 +315,35 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
   const int world = tr->world, me = tr->rank, d = p - e;
   if (world < 1 || me < 0 || me >= world) return sfail("transport world %d / rank %d invalid", world, me);
   if (L->nsets < 1 || !L->host || !L->slot || L->max_hosted < 1) return sfail("sharded layout: bad placement");
+  /* the column slice each process computes: the K computing processes in
+   * rank order take slices 0 .. K - 1 */
+  int* sidx = malloc(sizeof(int) * (size_t) world);
+  if (!sidx) return sfail("out of host memory");
+  int K = 0;
+  for (int g = 0; g < world; ++g) sidx[g] = (!compute || compute[g]) ? K++ : -1;
   const size_t W = L->slice_bytes;
-  if (W == 0 || W * (size_t) world < L->chunk_size) return sfail("slice_bytes %zu too small for %zu over %d", W,
-                                                                   L->chunk_size, world);
-  if (!L->hosted_data || !L->hosted_parity || !L->gathered_data || !L->gathered_parity)
+  if (K == 0 || W == 0 || W * (size_t) K < L->chunk_size) {
+    free(sidx);
+    return K == 0 ? sfail("sharded plan: no process computes")
+                  : sfail("slice_bytes %zu too small for %zu over %d", W, L->chunk_size, K);
+  }
+  if (!L->hosted_data || !L->hosted_parity || !L->gathered_data || !L->gathered_parity) {
+    free(sidx);
     return sfail("sharded layout: null buffer");
+  }
   const int nm = L->nsets * p, mh = L->max_hosted;
   {
     /* every (host, slot) at most once */
     unsigned char* used = calloc((size_t) world * mh, 1);
-    if (!used) return sfail("out of host memory");
+    if (!used) {
+      free(sidx);
+      return sfail("out of host memory");
+    }
     for (int m = 0; m < nm; ++m) {
       const int h = L->host[m], j = L->slot[m];
       if (h < 0 || h >= world || j < 0 || j >= mh || used[(size_t) h * mh + j]) {
         free(used);
+        free(sidx);
         return sfail("sharded layout: member %d placed at (%d, %d) invalid or twice", m, h, j);
       }
       used[(size_t) h * mh + j] = 1;
@@ -353,15 +373,15 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
   P->info.rank = me;
   P->info.nsets = L->nsets;
   P->info.missing = missing;
-  {
-    const size_t lo = (size_t) me * W;
+  if (sidx[me] >= 0) {
+    const size_t lo = (size_t) sidx[me] * W;
     P->info.my_slice_len = lo >= L->chunk_size ? 0 : (L->chunk_size - lo < W ? L->chunk_size - lo : W);
   }
   for (int i = 0; i < world * mh; ++i) by_slot[i] = -1;
   for (int m = 0; m < nm; ++m) by_slot[(size_t) L->host[m] * mh + L->slot[m]] = m;
   if ((rc = plan_inputs(rs, p, e, kind, missing, rebuild_ranks, need))) goto done;
 
-  pctx C = {L, by_slot, need, p, e, d, mh, world, me, kind, missing, P->lost, W};
+  pctx C = {L, by_slot, need, p, e, d, mh, world, me, kind, missing, P->lost, W, sidx, sidx[me]};
   P->goff = calloc((size_t) L->nsets + 1, sizeof(int));
   P->roff = calloc((size_t) L->nsets + 1, sizeof(int));
   if (!P->goff || !P->roff) {
@@ -389,7 +409,8 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
 
   /* compute: every set over my slices, cell stride W: a member hosted
    * elsewhere in the gathered layout, a member I host in place in its
-   * hosted slabs (my slice q = me is [d][W] / [e][W] there too) */
+   * hosted slabs (my slice q = sidx[me] is [d][W] / [e][W] there too); a
+   * process that computes nothing keeps no pointers */
   P->plans = calloc((size_t) L->nsets, sizeof(*P->plans));
   P->lofi = malloc(sizeof(*P->lofi) * (size_t) nm);
   P->parity = malloc(sizeof(*P->parity) * (size_t) nm);
@@ -398,9 +419,9 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
     goto done;
   }
   for (int m = 0; m < nm; ++m) {
-    const int local = L->host[m] == me;
-    P->lofi[m] = local ? hd(&C, me, L->slot[m], 0) : gd(&C, L->host[m], L->slot[m], 0);
-    P->parity[m] = local ? hp(&C, me, L->slot[m], 0) : gp(&C, L->host[m], L->slot[m], 0);
+    const int local = L->host[m] == me, q = C.me_s < 0 ? 0 : C.me_s;
+    P->lofi[m] = local ? hd(&C, q, L->slot[m], 0) : gd(&C, L->host[m], L->slot[m], 0);
+    P->parity[m] = local ? hp(&C, q, L->slot[m], 0) : gp(&C, L->host[m], L->slot[m], 0);
   }
   const size_t n = P->info.my_slice_len;
   P->info.compute_bytes = (unsigned long long) L->nsets * p * (d + (is_encode(kind) ? e : missing)) * n;
@@ -421,6 +442,7 @@ done:
   ex_free(&R);
   free(need);
   free(by_slot);
+  free(sidx);
   if (rc) {
     redset_hip_sharded_destroy(P);
     return REDSET_FAILURE;
@@ -429,9 +451,10 @@ done:
   return REDSET_SUCCESS;
 }
 
-int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
-                               const redset_hip_shard_layout* L, const redset_hip_transport* tr,
-                               const redset_hip_compute* comp, redset_hip_sharded** out) {
+int redset_hip_rs_sharded_plan_on(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
+                                  const redset_hip_shard_layout* L, const int* compute,
+                                  const redset_hip_transport* tr, const redset_hip_compute* comp,
+                                  redset_hip_sharded** out) {
   int p, e;
   if (!out) return sfail("sharded_plan: null out-pointer");
   *out = NULL;
@@ -439,12 +462,18 @@ int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, c
   if (redset_hip_rs_shape(rs, &p, &e)) return REDSET_FAILURE;
   if (kind != REDSET_HIP_PLAN_RS_ENCODE && kind != REDSET_HIP_PLAN_RS_REBUILD)
     return sfail("sharded_plan: kind %d is not RS encode or rebuild", kind);
-  return plan_sets(rs, p, e, kind, missing, rebuild_ranks, L, tr, comp, out);
+  return plan_sets(rs, p, e, kind, missing, rebuild_ranks, L, compute, tr, comp, out);
 }
 
-int redset_hip_xor_sharded_plan(int ranks, int kind, int root, const redset_hip_shard_layout* L,
-                                const redset_hip_transport* tr, const redset_hip_compute* comp,
-                                redset_hip_sharded** out) {
+int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
+                               const redset_hip_shard_layout* L, const redset_hip_transport* tr,
+                               const redset_hip_compute* comp, redset_hip_sharded** out) {
+  return redset_hip_rs_sharded_plan_on(rs, kind, missing, rebuild_ranks, L, NULL, tr, comp, out);
+}
+
+int redset_hip_xor_sharded_plan_on(int ranks, int kind, int root, const redset_hip_shard_layout* L,
+                                   const int* compute, const redset_hip_transport* tr,
+                                   const redset_hip_compute* comp, redset_hip_sharded** out) {
   if (!out) return sfail("xor_sharded_plan: null out-pointer");
   *out = NULL;
   if (!L || !tr || !tr->exchange) return sfail("xor_sharded_plan: null argument");
@@ -453,7 +482,14 @@ int redset_hip_xor_sharded_plan(int ranks, int kind, int root, const redset_hip_
     return sfail("xor_sharded_plan: kind %d is not XOR encode or rebuild", kind);
   if (kind == REDSET_HIP_PLAN_XOR_REBUILD && (root < 0 || root >= ranks))
     return sfail("root %d out of range", root);
-  return plan_sets(NULL, ranks, 1, kind, kind == REDSET_HIP_PLAN_XOR_REBUILD ? 1 : 0, &root, L, tr, comp, out);
+  return plan_sets(NULL, ranks, 1, kind, kind == REDSET_HIP_PLAN_XOR_REBUILD ? 1 : 0, &root, L, compute, tr, comp,
+                   out);
+}
+
+int redset_hip_xor_sharded_plan(int ranks, int kind, int root, const redset_hip_shard_layout* L,
+                                const redset_hip_transport* tr, const redset_hip_compute* comp,
+                                redset_hip_sharded** out) {
+  return redset_hip_xor_sharded_plan_on(ranks, kind, root, L, NULL, tr, comp, out);
 }
 
 static int compute_set(redset_hip_sharded* P, int k, void* stream) {

@@ -23,6 +23,10 @@
  * --gpu-host-null: the same on the null stream (the transport is
  * created for HIP-written host buffers, device_buffers = 2, and must wait for
  * the null stream too).
+ * SHARDED_TEST_IDLE=<r,r,...>: those processes compute no column slice
+ * (redset_hip_*_sharded_plan_on with the complementary mask; the others take
+ * slices 0 .. K - 1 of W = ceil(C / K)); they still host members, send their
+ * cells and receive their outputs.
  * Placement: `world` sets of p members, member m on process (m * 7 + 3) %
  * world (SHARDED_TEST_SEED=<s>: on a pseudo-random process), hosted slots in
  * ascending member order. Exit 0 iff every process
@@ -138,7 +142,19 @@ int main(int argc, char** argv) {
     slot[m] = count[host[m]]++;
     if (count[host[m]] > mh) mh = count[host[m]];
   }
-  const size_t W = redset_hip_shard_slice_bytes(C, world);
+  /* the processes that compute: all, or all but SHARDED_TEST_IDLE's */
+  int* on = malloc(sizeof(int) * world);
+  int NS = 0; /* column slices */
+  for (int g = 0; g < world; ++g) on[g] = 1;
+  if (getenv("SHARDED_TEST_IDLE")) {
+    char* list = strdup(getenv("SHARDED_TEST_IDLE"));
+    for (char* t = strtok(list, ","); t; t = strtok(NULL, ","))
+      if (atoi(t) >= 0 && atoi(t) < world) on[atoi(t)] = 0;
+    free(list);
+  }
+  for (int g = 0; g < world; ++g) NS += on[g];
+  if (NS == 0) MPI_Abort(MPI_COMM_WORLD, 2);
+  const size_t W = redset_hip_shard_slice_bytes(C, NS);
   const size_t hd = (size_t) world * mh * D * W, hp = (size_t) world * mh * E * W;
   uint8_t* HD = calloc(hd, 1);
   uint8_t* HP = calloc(hp, 1);
@@ -147,7 +163,7 @@ int main(int argc, char** argv) {
   /* my hosted members' slabs: slice q of data cell s */
   for (int m = 0; m < nm; ++m) {
     if (host[m] != me) continue;
-    for (int q = 0; q < world; ++q)
+    for (int q = 0; q < NS; ++q)
       for (int s = 0; s < D; ++s)
         for (size_t b = 0; b < W && q * W + b < C; ++b)
           HD[(((size_t) q * mh + slot[m]) * D + s) * W + b] = byte_of(m / P, m % P, s * C + q * W + b);
@@ -205,13 +221,13 @@ int main(int argc, char** argv) {
   int ok = (XOR || redset_hip_rs_create(P, E, &rs) == 0) &&
            redset_hip_mpi_transport_create(MPI_COMM_WORLD, host_slabs ? 2 : gpu ? 1 : 0, &tr, &th) == 0;
   if (ok && XOR)
-    ok = redset_hip_xor_sharded_plan(P, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, &tr, cp, &enc) == 0 &&
-         (missing == 0 ||
-          (missing == 1 && redset_hip_xor_sharded_plan(P, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, &tr, cp, &reb) == 0));
+    ok = redset_hip_xor_sharded_plan_on(P, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, on, &tr, cp, &enc) == 0 &&
+         (missing == 0 || (missing == 1 && redset_hip_xor_sharded_plan_on(P, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, on,
+                                                                            &tr, cp, &reb) == 0));
   else if (ok)
-    ok = redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, &tr, cp, &enc) == 0 &&
+    ok = redset_hip_rs_sharded_plan_on(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, on, &tr, cp, &enc) == 0 &&
          (missing == 0 ||
-          redset_hip_rs_sharded_plan(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, &tr, cp, &reb) == 0);
+          redset_hip_rs_sharded_plan_on(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, on, &tr, cp, &reb) == 0);
   if (!ok) fprintf(stderr, "rank %d: setup: %s\n", me, redset_hip_last_error());
   int bad = 0;
   if (ok && redset_hip_sharded_execute(enc, stream) != 0) {
@@ -222,7 +238,7 @@ int main(int argc, char** argv) {
   /* compare my hosted members' parity slabs with the oracle */
   for (int m = 0; ok && m < nm; ++m) {
     if (host[m] != me) continue;
-    for (int q = 0; q < world; ++q)
+    for (int q = 0; q < NS; ++q)
       for (int i = 0; i < E; ++i)
         for (size_t b = 0; b < W && q * W + b < C; ++b)
           bad += HP[(((size_t) q * mh + slot[m]) * E + i) * W + b] != want_p[m][i * C + q * W + b];
@@ -238,7 +254,7 @@ int main(int argc, char** argv) {
       int is_lost = 0;
       for (int i = 0; i < missing; ++i) is_lost |= lost[i] == m % P;
       if (!is_lost || host[m] != me) continue;
-      for (int q = 0; q < world; ++q) {
+      for (int q = 0; q < NS; ++q) {
         memset(HD + (((size_t) q * mh + slot[m]) * D) * W, 0xEE, (size_t) D * W);
         memset(HP + (((size_t) q * mh + slot[m]) * E) * W, 0xEE, (size_t) E * W);
       }
@@ -256,7 +272,7 @@ int main(int argc, char** argv) {
     int rbad = 0;
     for (int m = 0; ok && m < nm; ++m) {
       if (host[m] != me) continue;
-      for (int q = 0; q < world; ++q)
+      for (int q = 0; q < NS; ++q)
         for (size_t b = 0; b < W && q * W + b < C; ++b) {
           for (int s = 0; s < D; ++s)
             rbad += HD[(((size_t) q * mh + slot[m]) * D + s) * W + b] != want_l[m][s * C + q * W + b];
@@ -321,6 +337,7 @@ int main(int argc, char** argv) {
   free(GP);
   free(host);
   free(slot);
+  free(on);
   free(count);
   MPI_Finalize();
   return all ? 0 : 1;

@@ -65,6 +65,27 @@ def test_sharded_plan_random_shapes_and_placements(oracle, seed):
     assert res.stdout.count("rebuild gather") == np_
 
 
+@pytest.mark.parametrize("scheme,np_,p,e,chunk,lost,idle", [
+    ("rs", 4, 11, 3, 3001, [1, 2], "1"), ("rs", 4, 11, 3, 4096, [1, 2], "0,2"), ("rs", 3, 6, 2, 1000, [0, 4], "2"),
+    ("rs", 4, 20, 4, 777, [0, 5, 19], "3"), ("rs", 2, 6, 3, 1, [2], "0"), ("xor", 4, 5, 1, 999, [3], "1,3")])
+def test_sharded_plan_with_idle_processes(oracle, scheme, np_, p, e, chunk, lost, idle):
+    """redset_hip_{rs,xor}_sharded_plan_on: some processes compute no column
+    slice (the slot's host-slab decode keeps its lost members out of the
+    compute), the others take slices 0 .. K - 1 of ceil(C / K); every process
+    still hosts members, sends their cells and receives their outputs.
+    Parity after the encode and the lost members after the rebuild against the
+    oracle."""
+    if not _have():
+        pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", DRIVER, str(p), str(e), str(chunk)] + [str(x) for x in lost]
+    env = {**os.environ, "SHARDED_TEST_IDLE": idle}
+    if scheme == "xor":
+        env["SHARDED_TEST_SCHEME"] = "xor"
+    res = run_group(cmd, 120, env=env, cwd="/tmp")
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert res.stdout.count("rebuild gather") == np_
+
+
 @pytest.mark.parametrize("np_,p,chunk,root", [
     (2, 8, 3001, 3),     # configs[1]'s shape, small chunk
     (4, 4, 4096, 0),     # configs[0]'s set size

@@ -52,10 +52,14 @@ def _clean(res):
 @pytest.mark.parametrize("np_", [1, 2, 3, 4])
 @pytest.mark.parametrize("args", [(11, 3, 3001, 1, 2), (20, 4, 777, 0, 5, 19), (4, 2, 1, 0, 3), (5, 1, 65537, 4),
                                   (6, 2, 4096)])
-def test_sharded_planner_asan(asan_build, np_, args):
+@pytest.mark.parametrize("idle", ["", "0"])
+def test_sharded_planner_asan(asan_build, np_, args, idle):
+    """idle "0": process 0 computes no column slice (redset_hip_*_sharded_plan_on)"""
+    if idle and np_ == 1:
+        pytest.skip("someone must compute")
     cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", os.path.join(asan_build, "sharded_test")] + \
         [str(a) for a in args]
-    res = run_group(cmd, 180, env=ENV)
+    res = run_group(cmd, 180, env={**ENV, "SHARDED_TEST_IDLE": idle} if idle else ENV)
     assert _clean(res), res.stderr[-4000:]
     assert res.returncode == 0, res.stdout + res.stderr[-4000:]
 

@@ -145,6 +145,23 @@ int redset_hip_gf_combine(const unsigned char* const* in, int nin, unsigned char
 int redset_hip_xor_combine(const unsigned char* const* in, int nin, unsigned char* out,
                            size_t nbytes, int accumulate, void* stream);
 
+/* Many stripe combines of nbytes each as one plan (the gf_mac / xor kernels
+ * with the set plans' job orders: jobs of one shape share a launch): job k is
+ * out[j] = (out[j] ^) sum_i coef[j*nin + i] * in[i], as redset_hip_gf_combine;
+ * a job with one output and every coefficient 1 runs on the XOR kernel. No
+ * job's output may be another job's input. The arrays are copied; the
+ * buffers must outlive the plan. Used by the sharded plans' partial-sum
+ * shape (REDSET_HIP_SHAPE_REDUCE). */
+typedef struct {
+  int nin, nout;
+  const unsigned char* const* in;   /* nin device pointers */
+  unsigned char* const* out;        /* nout device pointers */
+  const unsigned char* coef;        /* nout x nin */
+  int accumulate;                   /* XOR into the outputs */
+} redset_hip_combine_job;
+int redset_hip_plan_combine(const redset_hip_combine_job* jobs, int njobs, size_t nbytes,
+                            redset_hip_plan** out);
+
 /* Host-side decode matrix for one stripe: rows = missing outputs, columns =
  * the p members (0 for erased members / unused cells). coef_out: missing x p
  * bytes. Equals the reference's reduce_decode + gaussian_solve as one linear
@@ -325,7 +342,18 @@ typedef struct {
 
 typedef struct redset_hip_sharded redset_hip_sharded;
 
-enum { REDSET_HIP_PHASE_GATHER = 0, REDSET_HIP_PHASE_COMPUTE = 1, REDSET_HIP_PHASE_RETURN = 2 };
+/* Phases of one execute, in this order. The gather shape: gather the input
+ * slices, compute, return the output slices (ACCUMULATE does nothing). The
+ * partial-sum shape (REDSET_HIP_SHAPE_REDUCE): GATHER does nothing, COMPUTE
+ * makes this process's partial sums, RETURN sends them to the outputs' hosts,
+ * ACCUMULATE adds what arrived (and this process's own inputs) into the
+ * outputs. Running the four in order is one execute in either shape. */
+enum {
+  REDSET_HIP_PHASE_GATHER = 0,
+  REDSET_HIP_PHASE_COMPUTE = 1,
+  REDSET_HIP_PHASE_RETURN = 2,
+  REDSET_HIP_PHASE_ACCUMULATE = 3
+};
 
 /* Column slice width for chunk_size bytes over `world` processes: ceil(C/world)
  * rounded up to 256 B (so every slice starts 16-B aligned). */
@@ -363,14 +391,72 @@ int redset_hip_rs_sharded_plan_on(const redset_hip_rs* rs, int kind, int missing
 int redset_hip_xor_sharded_plan_on(int ranks, int kind, int root, const redset_hip_shard_layout* layout,
                                    const int* compute_on, const redset_hip_transport* transport,
                                    const redset_hip_compute* compute, redset_hip_sharded** out);
-/* All three phases, ordered after the work already on `stream`; work
+/* The exchange's shape (redset_hip_sharded_opts.shape).
+ * GATHER: every computing process gathers its column slice of every cell a
+ *   stripe reads and returns its slice of every output -- (inputs + outputs)
+ *   x (world - 1) / world cells per stripe cross the fabric.
+ * REDUCE: the code is linear, so every process combines the inputs IT hosts
+ *   into partial outputs (the stripe's own coefficients) and sends one
+ *   partial per output and contributing process to the output's host, which
+ *   XORs them in: outputs x (contributing processes - 1) cells per stripe,
+ *   the shape of the reference's XOR ring, which moves partial sums
+ *   (src/redset_xor.c:251-279), where its RS decode gathers inputs
+ *   (src/redset_reedsolomon.c:690-733). The partials use the gathered slabs
+ *   as scratch; a plan whose partials do not fit them, or with over 64
+ *   processes, cannot take it.
+ * AUTO: whichever moves fewer bytes through the busiest process (max over
+ *   processes of max(bytes sent, bytes received) per execute; ties: GATHER).
+ *   Every process computes every process's counts, so all choose alike. */
+enum { REDSET_HIP_SHAPE_AUTO = 0, REDSET_HIP_SHAPE_GATHER = 1, REDSET_HIP_SHAPE_REDUCE = 2 };
+
+typedef struct {
+  size_t struct_size;             /* sizeof(redset_hip_sharded_opts): checked */
+  int shape;                      /* REDSET_HIP_SHAPE_* */
+  const int* compute_on;          /* as redset_hip_rs_sharded_plan_on (GATHER only; NULL = all) */
+  const redset_hip_compute* compute; /* whole-set compute callback (GATHER; NULL = HIP plans) */
+  /* the REDUCE shape's compute callback (NULL = HIP plans, redset_hip_plan_combine):
+   * run the `njobs` combines of one phase of one set, each over nbytes */
+  int (*combine)(void* ctx, const redset_hip_combine_job* jobs, int njobs, size_t nbytes, void* stream);
+  void* combine_ctx;
+} redset_hip_sharded_opts;
+
+/* The plans above with options: the exchange's shape and the callbacks. The
+ * four-argument forms above are this with shape GATHER (their callers run the
+ * gather shape's phases themselves, e.g. the per-rank slot). AUTO (or REDUCE)
+ * with a whole-set `compute` callback and no `combine` plans GATHER. */
+int redset_hip_rs_sharded_plan_ex(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
+                                  const redset_hip_shard_layout* layout, const redset_hip_transport* transport,
+                                  const redset_hip_sharded_opts* opts, redset_hip_sharded** out);
+int redset_hip_xor_sharded_plan_ex(int ranks, int kind, int root, const redset_hip_shard_layout* layout,
+                                   const redset_hip_transport* transport, const redset_hip_sharded_opts* opts,
+                                   redset_hip_sharded** out);
+
+/* Both shapes' byte counts and the one planned. */
+typedef struct {
+  size_t struct_size;                       /* set by the library */
+  int shape;                                /* REDSET_HIP_SHAPE_GATHER or _REDUCE */
+  int reduce_possible;                      /* the partial sums fit the scratch */
+  unsigned long long gather_busiest_bytes;  /* max over processes of max(sent, received), per execute */
+  unsigned long long reduce_busiest_bytes;  /* the same for REDUCE (0 if not possible) */
+  unsigned long long gather_bytes_sent, gather_bytes_recv;  /* this process, GATHER */
+  unsigned long long reduce_bytes_sent, reduce_bytes_recv;  /* this process, REDUCE */
+  unsigned long long scratch_bytes_needed;  /* REDUCE: this process's partial-sum rows */
+  unsigned long long scratch_bytes;         /* the gathered slabs */
+  int reduce_messages, reduce_recv_messages; /* REDUCE: peer messages per execute, after merging */
+} redset_hip_sharded_shape_info;
+/* Copies min(size, sizeof) bytes: callers built against an older header get
+ * the fields they know, never a write past their struct. */
+int redset_hip_sharded_get_shape(const redset_hip_sharded* plan, redset_hip_sharded_shape_info* info, size_t size);
+
+/* All phases, ordered after the work already on `stream`; work
  * enqueued on `stream` afterwards sees the results. With the HIP plans as
  * compute (compute == NULL at plan time) the sets are pipelined: every set's
  * gather and return is an exchange of its own on a second stream the plan
  * owns, so set k+1's gather (and the first returns) overlap set k's gf_mac on
  * `stream`. With a compute callback the phases run one after another. */
 int redset_hip_sharded_execute(redset_hip_sharded* plan, void* stream);
-/* One phase (REDSET_HIP_PHASE_*), so callers can time them apart. */
+/* One phase (REDSET_HIP_PHASE_*), so callers can time them apart; the four in
+ * order are one execute. */
 int redset_hip_sharded_execute_phase(redset_hip_sharded* plan, int phase, void* stream);
 int redset_hip_sharded_get_info(const redset_hip_sharded* plan, redset_hip_sharded_info* info);
 void redset_hip_sharded_destroy(redset_hip_sharded* plan);
@@ -432,6 +518,15 @@ const char* redset_hip_last_error(void);
 int redset_hip_record_error(const char* msg);
 /* Library version string. */
 const char* redset_hip_version(void);
+/* The revision of this header's struct layouts (REDSET_HIP_ABI_VERSION) the
+ * library was built with. It changes whenever a struct that crosses this
+ * ABI changes size or layout; a caller compares it with the header it was
+ * built against and refuses to run on a mismatch (the Python binding and the
+ * per-rank backends do), so a stale caller fails loudly instead of writing
+ * past a struct. 6: round 6 (combine jobs, sharded options and
+ * shape info; PHASE_ACCUMULATE). */
+#define REDSET_HIP_ABI_VERSION 6
+int redset_hip_abi_version(void);
 
 #ifdef __cplusplus
 }

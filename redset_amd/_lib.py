@@ -71,11 +71,27 @@ EXPORTED_SYMBOLS = (
     "redset_hip_rccl_unique_id",
     "redset_hip_rccl_transport_create",
     "redset_hip_rccl_transport_destroy",
+    "redset_hip_plan_combine",
+    "redset_hip_rs_sharded_plan_ex",
+    "redset_hip_xor_sharded_plan_ex",
+    "redset_hip_sharded_get_shape",
+    "redset_hip_abi_version",
 )
+
+# include/redset_hip.h REDSET_HIP_ABI_VERSION: the struct layouts below
+ABI_VERSION = 6
 
 PHASE_GATHER = 0
 PHASE_COMPUTE = 1
 PHASE_RETURN = 2
+PHASE_ACCUMULATE = 3
+# every phase of one execute, in order (either shape)
+PHASES = (PHASE_GATHER, PHASE_COMPUTE, PHASE_RETURN, PHASE_ACCUMULATE)
+
+SHAPE_AUTO = 0
+SHAPE_GATHER = 1
+SHAPE_REDUCE = 2
+SHAPE_NAMES = {SHAPE_AUTO: "auto", SHAPE_GATHER: "gather", SHAPE_REDUCE: "reduce"}
 
 
 class RedsetHipUnavailable(RuntimeError):
@@ -132,12 +148,50 @@ COMPUTE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, c_int, c_int, POINTER(c_int), POI
                               c_size_t, c_size_t, c_void_p)
 
 
+class CombineJob(ctypes.Structure):
+    """redset_hip_combine_job: out[j] = (out[j] ^) sum_i coef[j*nin+i] * in[i]."""
+
+    _fields_ = [("nin", c_int), ("nout", c_int), ("inp", POINTER(c_void_p)), ("out", POINTER(c_void_p)),
+                ("coef", POINTER(c_ubyte)), ("accumulate", c_int)]
+
+
+COMBINE_FN = ctypes.CFUNCTYPE(c_int, c_void_p, POINTER(CombineJob), c_int, c_size_t, c_void_p)
+
+
 class Transport(ctypes.Structure):
     _fields_ = [("world", c_int), ("rank", c_int), ("exchange", c_void_p), ("ctx", c_void_p)]
 
 
 class Compute(ctypes.Structure):
     _fields_ = [("run", c_void_p), ("ctx", c_void_p)]
+
+
+class ShardedOpts(ctypes.Structure):
+    _fields_ = [("struct_size", c_size_t), ("shape", c_int), ("compute_on", POINTER(c_int)),
+                ("compute", POINTER(Compute)), ("combine", c_void_p), ("combine_ctx", c_void_p)]
+
+
+class ShapeInfo(ctypes.Structure):
+    _fields_ = [
+        ("struct_size", c_size_t),
+        ("shape", c_int),
+        ("reduce_possible", c_int),
+        ("gather_busiest_bytes", c_ulonglong),
+        ("reduce_busiest_bytes", c_ulonglong),
+        ("gather_bytes_sent", c_ulonglong),
+        ("gather_bytes_recv", c_ulonglong),
+        ("reduce_bytes_sent", c_ulonglong),
+        ("reduce_bytes_recv", c_ulonglong),
+        ("scratch_bytes_needed", c_ulonglong),
+        ("scratch_bytes", c_ulonglong),
+        ("reduce_messages", c_int),
+        ("reduce_recv_messages", c_int),
+    ]
+
+    def as_dict(self):
+        d = {k: getattr(self, k) for k, _ in self._fields_ if k != "struct_size"}
+        d["shape"] = SHAPE_NAMES.get(d["shape"], d["shape"])
+        return d
 
 
 class ShardLayout(ctypes.Structure):
@@ -238,6 +292,15 @@ _SIGNATURES = {
     "redset_hip_sharded_execute_phase": (c_int, [c_void_p, c_int, c_void_p]),
     "redset_hip_sharded_get_info": (c_int, [c_void_p, POINTER(ShardedInfo)]),
     "redset_hip_sharded_destroy": (None, [c_void_p]),
+    "redset_hip_plan_combine": (c_int, [POINTER(CombineJob), c_int, c_size_t, POINTER(c_void_p)]),
+    "redset_hip_rs_sharded_plan_ex": (
+        c_int, [c_void_p, c_int, c_int, POINTER(c_int), POINTER(ShardLayout), POINTER(Transport), POINTER(ShardedOpts),
+                POINTER(c_void_p)]),
+    "redset_hip_xor_sharded_plan_ex": (
+        c_int, [c_int, c_int, c_int, POINTER(ShardLayout), POINTER(Transport), POINTER(ShardedOpts),
+                POINTER(c_void_p)]),
+    "redset_hip_sharded_get_shape": (c_int, [c_void_p, POINTER(ShapeInfo), c_size_t]),
+    "redset_hip_abi_version": (c_int, []),
     "redset_hip_rccl_available": (c_int, []),
     "redset_hip_rccl_unique_id": (c_int, [POINTER(c_ubyte)]),
     "redset_hip_rccl_transport_create": (c_int, [POINTER(c_ubyte), c_int, c_int, POINTER(Transport), POINTER(c_void_p)]),
@@ -279,6 +342,12 @@ def open_library(path: str) -> ctypes.CDLL:
         fn = getattr(lib, name)
         fn.restype = res
         fn.argtypes = args
+    got = lib.redset_hip_abi_version()
+    if got != ABI_VERSION:
+        # the struct layouts bound above belong to another header revision:
+        # fail loudly instead of reading or writing past a struct
+        raise RedsetHipUnavailable(f"{path} has ABI version {got}, this binding expects {ABI_VERSION} "
+                                   "(rebuild: make -C redset_amd/csrc)")
     return lib
 
 

@@ -406,6 +406,12 @@ static int injected_device_failure(MPI_Comm comm) {
 static int comm_geometry(MPI_Comm comm, int* ranks, int* rank) {
   if (MPI_Comm_size(comm, ranks) != MPI_SUCCESS || MPI_Comm_rank(comm, rank) != MPI_SUCCESS)
     return fail("MPI_Comm_size/rank failed");
+  /* the codec library's struct layouts are the ones this file was built
+   * against (every member loads the same library, so every member returns
+   * here alike, before any collective) */
+  if (redset_hip_abi_version() != REDSET_HIP_ABI_VERSION)
+    return fail("libredset_hip has ABI version %d, the backends were built for %d", redset_hip_abi_version(),
+                REDSET_HIP_ABI_VERSION);
   return 0;
 }
 
@@ -1198,7 +1204,7 @@ static void slot_ctx_free(slot_ctx* C) {
 /* per-communicator exchange, decided once and cached on the communicator
  * (an MPI attribute: the RCCL communicator, a _SHARDED_MPI transport and the
  * slot context are destroyed with it) */
-typedef struct {
+typedef struct comm_exchange {
   int decided;             /* the RCCL decision has been made */
   int mode;                /* REDSET_HIP_EXCHANGE_HOST_MPI or _SHARDED_RCCL */
   redset_hip_transport tr;
@@ -1209,22 +1215,27 @@ typedef struct {
   redset_hip_mpi_transport* ht;
   slot_ctx* ctx;
   int busy;                /* a sharded call is using mt / ctx (under exch_mu) */
+  struct comm_exchange* next; /* the live list (exch_register) */
 } comm_exchange;
 
 /* every live comm_exchange, so redset_hip_rank_scratch_release can free
- * what they cache */
-#define MAX_EXCH 64
+ * what they cache: an intrusive list, so no communicator is ever left out
+ * (a fixed table of 64 dropped the 65th silently) */
 static pthread_mutex_t exch_mu = PTHREAD_MUTEX_INITIALIZER;
-static comm_exchange* exch_live[MAX_EXCH];
+static comm_exchange* exch_head;
 
 static void exch_register(comm_exchange* X, int add) {
   pthread_mutex_lock(&exch_mu);
-  for (int i = 0; i < MAX_EXCH; ++i) {
-    if (add && !exch_live[i]) {
-      exch_live[i] = X;
-      break;
-    }
-    if (!add && exch_live[i] == X) exch_live[i] = NULL;
+  if (add) {
+    X->next = exch_head;
+    exch_head = X;
+  } else {
+    for (comm_exchange** pp = &exch_head; *pp; pp = &(*pp)->next)
+      if (*pp == X) {
+        *pp = X->next;
+        break;
+      }
+    X->next = NULL;
   }
   pthread_mutex_unlock(&exch_mu);
 }
@@ -1408,8 +1419,8 @@ static int choose_exchange_now(MPI_Comm comm, int p, int r, int autop, int* mode
  * holds the transport and the context */
 static void exch_release_all(void) {
   pthread_mutex_lock(&exch_mu);
-  for (int i = 0; i < MAX_EXCH; ++i)
-    if (exch_live[i] && !exch_live[i]->busy) exch_release(exch_live[i]);
+  for (comm_exchange* X = exch_head; X; X = X->next)
+    if (!X->busy) exch_release(X);
   pthread_mutex_unlock(&exch_mu);
 }
 
@@ -1558,14 +1569,20 @@ static slot_ctx* slot_ctx_get(comm_exchange* X, int host_slabs, const redset_hip
 }
 
 /* cell bytes per window of the sharded slot: `budget` over the p cells a
- * member holds, at least one MPI buffer, at most the chunk */
+ * member holds (4 KiB multiples, at least 64 KiB), at most the chunk. The
+ * caller's MPI buffer size does not raise it: the window sizes every pinned
+ * image and slab of the call (host slabs: two sets of hosted + gathered
+ * slabs, ~4 p win), and a window raised to a 64 MiB buffer pinned 2.8 GiB per
+ * member for RS(8+3); the messages are the window's column
+ * slices, not MPI buffers, so B has no say in them */
 static size_t slot_window(size_t budget, size_t chunk_size, int ncell, size_t B) {
-  size_t win = budget / (size_t) ncell;
+  (void) B;
+  size_t win = budget / (size_t) ncell / 4096 * 4096;
+  if (win < ((size_t) 64 << 10)) win = (size_t) 64 << 10;
 #if REDSET_HIP_TEST_KNOBS
   /* test builds: small windows, so small sets take several (the mid-call stop) */
   if (getenv("REDSET_HIP_TEST_SHARDED_WINDOW")) win = (size_t) atoll(getenv("REDSET_HIP_TEST_SHARDED_WINDOW"));
 #endif
-  if (win < B) win = B;
   if (win > chunk_size) win = chunk_size;
   if (win == 0) win = 1;
   return win;
@@ -1625,9 +1642,12 @@ static int sharded_slot_host(int encode, const redset_hip_rs* rs, MPI_Comm comm,
     redset_hip_sharded* P = n < nwin ? C->plan[b][WIN_LEN(n) != win] : NULL;
     redset_hip_sharded* Pp = n >= 1 ? C->plan[pb][WIN_LEN(n - 1) != win] : NULL;
     if (n < nwin) {
-      /* window n into slabs b (last used by window n - 2, whose kernels,
-       * return and writes are done) */
+      /* window n into slabs b, last used by window n - 2: its return and
+       * writes are done (iteration n - 1), and its kernels are waited for
+       * here, not left to the return's stream sync as a side effect (a
+       * member with no return traffic never syncs it) */
       const size_t off = n * win, len = WIN_LEN(n);
+      if (n >= 2 && !rc && ev_wait(C->ev[b])) rc = REDSET_FAILURE;
       for (int x = 0; x < ncell && !rc; ++x) {
         if (!C->want[x]) continue;
         for (size_t q = 0; q < (size_t) world && q * W < len && !rc; ++q) {

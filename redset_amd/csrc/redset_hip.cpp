@@ -198,8 +198,9 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
     std::vector<XorJob> jobs;
     int nin, accumulate, bytes_only;
   };
-  std::map<std::tuple<int, int, int, int>, GfPending> gf;  // (input group, nin, nout, unaligned)
-  std::map<std::tuple<int, int, int>, XorPending> xr;      // (input group, nin, unaligned)
+  // (input group, nin, nout, unaligned, accumulate) / (input group, nin, unaligned, accumulate)
+  std::map<std::tuple<int, int, int, int, int>, GfPending> gf;
+  std::map<std::tuple<int, int, int, int>, XorPending> xr;
   unsigned long long rd = 0, wr = 0;
   for (const StripeMap& m : maps) {
     const int nin = static_cast<int>(m.in.size());
@@ -212,7 +213,8 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
       for (int ig = 0; ig * kMaxIn < nin; ++ig) {
         const int i0 = ig * kMaxIn, ni = std::min(kMaxIn, nin - i0);
         bool al = true;
-        rd += static_cast<unsigned long long>(ni + (ig > 0 ? no : 0)) * nbytes;
+        const int acc = ig > 0 || m.accumulate;
+        rd += static_cast<unsigned long long>(ni + (acc ? no : 0)) * nbytes;
         wr += static_cast<unsigned long long>(no) * nbytes;
         if (m.xor_only) {
           XorJob J;
@@ -223,9 +225,9 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
           }
           J.out = L.at(m.out[o0]);
           al = al && aligned16(J.out);
-          XorPending& P = xr[std::make_tuple(ig, ni, al ? 0 : 1)];
+          XorPending& P = xr[std::make_tuple(ig, ni, al ? 0 : 1, acc)];
           P.nin = ni;
-          P.accumulate = ig > 0;
+          P.accumulate = acc;
           P.bytes_only = al ? 0 : 1;
           P.jobs.push_back(J);
           continue;
@@ -241,10 +243,10 @@ int build_plan(redset_hip_plan* plan, const std::vector<StripeMap>& maps, const 
           al = al && aligned16(J.out[j]);
           for (int i = 0; i < ni; ++i) J.coef[j][i] = m.coef[static_cast<size_t>(o0 + j) * nin + i0 + i];
         }
-        GfPending& P = gf[std::make_tuple(ig, ni, no, al ? 0 : 1)];
+        GfPending& P = gf[std::make_tuple(ig, ni, no, al ? 0 : 1, acc)];
         P.nin = ni;
         P.nout = no;
-        P.accumulate = ig > 0;
+        P.accumulate = acc;
         P.bytes_only = al ? 0 : 1;
         P.jobs.push_back(J);
       }
@@ -443,7 +445,8 @@ int redset_hip_rs_shape(const redset_hip_rs* rs, int* ranks, int* encoding) {
   if (encoding) *encoding = rs->encoding;
   return REDSET_SUCCESS;
 }
-const char* redset_hip_version(void) { return "redset-hip 0.2 (gfx950)"; }
+const char* redset_hip_version(void) { return "redset-hip 0.3 (gfx950)"; }
+int redset_hip_abi_version(void) { return REDSET_HIP_ABI_VERSION; }
 
 int redset_hip_rs_create(int ranks, int encoding, redset_hip_rs** out) {
   if (!out) return fail("null out-pointer");
@@ -547,6 +550,39 @@ int redset_hip_xor_plan_rebuild(int ranks, int root, unsigned char* const* lofi,
   std::vector<StripeMap> maps(ranks);
   for (int c = 0; c < ranks; ++c) redset_hip::xor_rebuild_map(ranks, root, c, maps[c]);
   return finish_plan(REDSET_HIP_PLAN_XOR_REBUILD, ranks, 1, 1, chunk_size, maps, SetLayout{lofi, xorc, stride}, out);
+}
+
+int redset_hip_plan_combine(const redset_hip_combine_job* jobs, int njobs, size_t nbytes, redset_hip_plan** out) {
+  if (!out) return fail("plan_combine: null out-pointer");
+  *out = nullptr;
+  if (njobs < 0 || (njobs > 0 && !jobs)) return fail("plan_combine: bad job list");
+  // every job's cells as entries of one pointer table, so the set planner
+  // (build_plan) takes them as cells of a layout with stride 0: cell
+  // (rank = table index, index 0)
+  std::vector<unsigned char*> table;
+  std::vector<StripeMap> maps(static_cast<size_t>(njobs));
+  for (int k = 0; k < njobs; ++k) {
+    const redset_hip_combine_job& J = jobs[k];
+    if (J.nin < 1 || J.nin > kMaxCombine || J.nout < 1 || J.nout > kMaxCombine || !J.in || !J.out || !J.coef)
+      return fail("plan_combine: job %d: nin=%d, nout=%d (1..%d) or null array", k, J.nin, J.nout, kMaxCombine);
+    StripeMap& m = maps[static_cast<size_t>(k)];
+    bool ones = J.nout == 1;
+    for (int i = 0; i < J.nin; ++i) {
+      if (!J.in[i]) return fail("plan_combine: job %d: null input %d", k, i);
+      m.in.push_back(redset_hip::CellRef{static_cast<int>(table.size()), redset_hip::kData, 0});
+      table.push_back(const_cast<unsigned char*>(J.in[i]));
+    }
+    for (int j = 0; j < J.nout; ++j) {
+      if (!J.out[j]) return fail("plan_combine: job %d: null output %d", k, j);
+      m.out.push_back(redset_hip::CellRef{static_cast<int>(table.size()), redset_hip::kData, 0});
+      table.push_back(J.out[j]);
+    }
+    m.coef.assign(J.coef, J.coef + static_cast<size_t>(J.nin) * J.nout);
+    for (uint8_t c : m.coef) ones = ones && c == 1;
+    m.xor_only = ones;  // one output, every coefficient 1: the XOR kernel
+    m.accumulate = J.accumulate != 0;
+  }
+  return finish_plan(0, 0, 0, 0, nbytes, maps, SetLayout{table.data(), table.data(), 0}, out);
 }
 
 int redset_hip_plan_execute(const redset_hip_plan* plan, void* stream) {

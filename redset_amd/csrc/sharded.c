@@ -129,6 +129,80 @@ static int ex_flatten(exch* X, xlist* out, const xstats* st) {
   return 0;
 }
 
+/* ---- combine job lists (the partial-sum shape) -------------------------- */
+
+/* jobs with their pointer and coefficient arrays in growing pools; the jobs
+ * keep pool offsets until cs_finish points them at the pools */
+typedef struct {
+  redset_hip_combine_job* v;
+  int n, cap;
+  unsigned char** ptr;             /* inputs then outputs of every job */
+  size_t np, pcap;
+  unsigned char* coef;
+  size_t nc, ccap;
+  unsigned long long bytes;        /* HBM bytes the jobs move (reads + writes) */
+} cset;
+
+static void cs_free(cset* S) {
+  free(S->v);
+  free(S->ptr);
+  free(S->coef);
+  memset(S, 0, sizeof(*S));
+}
+
+/* one job: nin inputs, nout outputs, coef nout x nin, over n cell bytes */
+static int cs_add(cset* S, int nin, unsigned char* const* in, int nout, unsigned char* const* out,
+                  const unsigned char* coef, int accumulate, size_t n) {
+  if (S->n == S->cap) {
+    int cap = S->cap ? 2 * S->cap : 32;
+    redset_hip_combine_job* v = realloc(S->v, sizeof(*v) * (size_t) cap);
+    if (!v) return sfail("out of host memory");
+    S->v = v;
+    S->cap = cap;
+  }
+  const size_t k = (size_t) nin + (size_t) nout, kc = (size_t) nin * (size_t) nout;
+  if (S->np + k > S->pcap) {
+    size_t cap = S->pcap ? 2 * S->pcap : 256;
+    while (cap < S->np + k) cap *= 2;
+    unsigned char** v = realloc(S->ptr, sizeof(*v) * cap);
+    if (!v) return sfail("out of host memory");
+    S->ptr = v;
+    S->pcap = cap;
+  }
+  if (S->nc + kc > S->ccap) {
+    size_t cap = S->ccap ? 2 * S->ccap : 1024;
+    while (cap < S->nc + kc) cap *= 2;
+    unsigned char* v = realloc(S->coef, cap);
+    if (!v) return sfail("out of host memory");
+    S->coef = v;
+    S->ccap = cap;
+  }
+  redset_hip_combine_job J;
+  J.nin = nin;
+  J.nout = nout;
+  J.in = (const unsigned char* const*) (uintptr_t) S->np; /* offsets until cs_finish */
+  J.out = (unsigned char* const*) (uintptr_t) (S->np + (size_t) nin);
+  J.coef = (const unsigned char*) (uintptr_t) S->nc;
+  J.accumulate = accumulate;
+  memcpy(S->ptr + S->np, in, sizeof(*in) * (size_t) nin);
+  memcpy(S->ptr + S->np + nin, out, sizeof(*out) * (size_t) nout);
+  memcpy(S->coef + S->nc, coef, kc);
+  S->np += k;
+  S->nc += kc;
+  S->v[S->n++] = J;
+  S->bytes += (unsigned long long) (nin + nout + (accumulate ? nout : 0)) * n;
+  return 0;
+}
+
+static void cs_finish(cset* S) {
+  for (int i = 0; i < S->n; ++i) {
+    redset_hip_combine_job* J = &S->v[i];
+    J->in = (const unsigned char* const*) (S->ptr + (uintptr_t) J->in);
+    J->out = S->ptr + (uintptr_t) J->out;
+    J->coef = S->coef + (uintptr_t) J->coef;
+  }
+}
+
 /* ---- the plan ---------------------------------------------------------- */
 
 struct redset_hip_sharded {
@@ -151,6 +225,19 @@ struct redset_hip_sharded {
   redset_hip_plan** plans;         /* [nsets] (NULL entries when my slice is empty) */
   unsigned char** lofi;            /* [nsets * p] */
   unsigned char** parity;          /* [nsets * p] */
+  /* the partial-sum shape (REDSET_HIP_SHAPE_REDUCE): per set, the combines
+   * of the COMPUTE phase (partial sums, and outputs only my inputs feed) and
+   * of the ACCUMULATE phase (outputs partials arrived for); the partial
+   * exchange is `ret` */
+  int shape;
+  cset* part;                      /* [nsets] */
+  cset* acc;                       /* [nsets] */
+  redset_hip_plan** part_plans;    /* [nsets] (HIP compute; NULL: no job) */
+  redset_hip_plan** acc_plans;     /* [nsets] */
+  hipEvent_t* ev_r;                /* [nsets] set k's partials arrived */
+  int (*combine)(void*, const redset_hip_combine_job*, int, size_t, void*);
+  void* combine_ctx;
+  redset_hip_sharded_shape_info shape_info;
 };
 
 size_t redset_hip_shard_slice_bytes(size_t chunk_size, int world) {
@@ -299,11 +386,450 @@ static int plan_return(const pctx* C, int k, exch* R) {
   return rc;
 }
 
+/* ---- the partial-sum shape (REDSET_HIP_SHAPE_REDUCE) ------------------- */
+/*
+ * Every output cell O of a stripe (a lost member's cell; encode: a parity
+ * cell) is a linear combination of the stripe's input cells. The processes
+ * hosting some input with a nonzero coefficient for O are O's contributors;
+ * each one other than O's host combines ITS inputs into a partial cell and
+ * sends it to O's host, which XORs the partials and its own inputs' share
+ * into O. GF(2^8) addition is XOR, so the bytes equal the whole combination's
+ * (the reference's multadd, src/redset_reedsolomon_common.c:786-819, sums in
+ * another order to the same bytes).
+ *
+ * Slice by slice: a member's cells are stored as `world` column slabs, so
+ * every combine works on one slice q of its cells (W bytes; the last slice's
+ * padding is computed and sent too, and lands in padding). A partial's slice
+ * q is a row of W bytes: in the sender's scratch (the gathered slabs, which
+ * this shape does not otherwise use), and at the receiver either straight in
+ * the output (the first remote contributor's, in rank order) or in the
+ * receiver's scratch (the others'), from where the ACCUMULATE combine XORs
+ * it in.
+ *
+ * Every process computes the same row allocation for every process, so a
+ * pair's messages merge rows alike on both sides: a sender's rows for
+ * receiver h, set k, lie in its scratch in the order (q, output); a
+ * receiver's rows from sender g, set k, likewise; rows merge into one
+ * message where both sides are contiguous.
+ */
+#define REDUCE_MAX_WORLD 64
+
+typedef struct {
+  int r, pass, x, c; /* member of the set, 0: data cell x / 1: parity slot x, stripe */
+} ocell;
+
+/* every output cell of a set (the same in every set) and its stripe's
+ * coefficients over the p members, coef[o * p + s] */
+static int set_outputs(const redset_hip_rs* rs, int p, int e, int kind, int missing, const int* lost, ocell** oc_out,
+                       unsigned char** coef_out, int* nout_out) {
+  const int per = is_encode(kind) ? e : missing;
+  const int n = p * per;
+  ocell* oc = malloc(sizeof(*oc) * (size_t) n);
+  unsigned char* coef = calloc((size_t) n * p, 1);
+  unsigned char* mat = rs ? malloc((size_t) (p + e) * p) : NULL;
+  unsigned char* D = malloc((size_t) (missing > 0 ? missing : 1) * p);
+  int rc = (!oc || !coef || !D || (rs && !mat)) ? sfail("out of host memory") : 0;
+  if (!rc && rs) rc = redset_hip_rs_matrix(rs, mat);
+  int o = 0;
+  for (int c = 0; c < p && !rc; ++c) {
+    if (kind == REDSET_HIP_PLAN_RS_REBUILD && (rc = redset_hip_rs_decode_matrix(rs, missing, lost, c, D))) break;
+    for (int i = 0; i < p && o < n; ++i) {
+      int r = -1;
+      if (kind == REDSET_HIP_PLAN_RS_ENCODE) {
+        if (redset_hip_rs_get_encoding_id(p, e, i, c) >= p) r = i;
+      } else if (kind == REDSET_HIP_PLAN_XOR_ENCODE) {
+        if (i == c) r = c;
+      } else if (i < missing) {
+        r = lost[i];
+      }
+      if (r < 0) continue;
+      const int x = cell_of(p, e, kind, r, c);
+      ocell O = {r, x >= 0 ? 0 : 1, x >= 0 ? x : -(1 + x), c};
+      oc[o] = O;
+      unsigned char* row = coef + (size_t) o * p;
+      for (int t = 0; t < p; ++t) {
+        if (kind == REDSET_HIP_PLAN_RS_ENCODE) {
+          const int enc = redset_hip_rs_get_encoding_id(p, e, r, c);
+          row[t] = redset_hip_rs_get_encoding_id(p, e, t, c) < p ? mat[(size_t) enc * p + t] : 0;
+        } else if (kind == REDSET_HIP_PLAN_RS_REBUILD) {
+          row[t] = D[(size_t) i * p + t];
+        } else {
+          row[t] = t != r;
+        }
+      }
+      ++o;
+    }
+  }
+  free(mat);
+  free(D);
+  if (!rc && o != n) rc = sfail("sharded plan: %d outputs per set, expected %d", o, n);
+  if (rc) {
+    free(oc);
+    free(coef);
+    return REDSET_FAILURE;
+  }
+  *oc_out = oc;
+  *coef_out = coef;
+  *nout_out = n;
+  return 0;
+}
+
+/* the row allocation of the partial-sum shape for every process */
+typedef struct {
+  int world, nsets, nout, p, d, e, mh;
+  size_t W, C;
+  int nslices;              /* slices with cell bytes */
+  const int *host, *slot;   /* layout placement */
+  ocell* oc;
+  unsigned char* coef;
+  int* ord;                 /* [nsets][nout] set k's outputs by (pass, slot, cell) */
+  uint64_t* mask;           /* [nsets][nout] contributing processes */
+  long* srow;               /* [k][o][q][g] row of sender g's scratch, or -1 */
+  long* rrow;               /* [k][o][q][g] row of the receiver's scratch, -1 (direct) */
+  long *S, *R;              /* [world] scratch rows sent / received into scratch */
+  unsigned long long *sent, *recvd; /* [world] rows sent / received */
+  long rows;                /* scratch rows per process (the gathered slabs) */
+  int ok;                   /* fits, and every output has a contributor */
+} reduce_alloc;
+
+static void ra_free(reduce_alloc* A) {
+  free(A->oc);
+  free(A->coef);
+  free(A->ord);
+  free(A->mask);
+  free(A->srow);
+  free(A->rrow);
+  free(A->S);
+  free(A->R);
+  free(A->sent);
+  free(A->recvd);
+  memset(A, 0, sizeof(*A));
+}
+
+static size_t ra_key(const reduce_alloc* A, int k, int o, int q, int g) {
+  return (((size_t) k * A->nout + o) * (size_t) A->world + (size_t) q) * (size_t) A->world + (size_t) g;
+}
+static int ra_host(const reduce_alloc* A, int k, int o) { return A->host[(size_t) k * A->p + A->oc[o].r]; }
+static int ra_slot(const reduce_alloc* A, int k, int o) { return A->slot[(size_t) k * A->p + A->oc[o].r]; }
+/* O's contributors other than its host */
+static uint64_t ra_remote(const reduce_alloc* A, int k, int o) {
+  return A->mask[(size_t) k * A->nout + o] & ~((uint64_t) 1 << ra_host(A, k, o));
+}
+
+/* set k's outputs by (pass, the host's slot, cell): the order of a pair's rows */
+static int ra_before(const reduce_alloc* A, int k, int oa, int ob) {
+  const ocell *x = &A->oc[oa], *y = &A->oc[ob];
+  if (x->pass != y->pass) return x->pass < y->pass;
+  const int sa = ra_slot(A, k, oa), sb = ra_slot(A, k, ob);
+  if (sa != sb) return sa < sb;
+  return x->x < y->x;
+}
+static void ra_sort(const reduce_alloc* A, int k, int* v, int n) {
+  for (int i = 1; i < n; ++i) {
+    const int t = v[i];
+    int j = i;
+    for (; j > 0 && ra_before(A, k, t, v[j - 1]); --j) v[j] = v[j - 1];
+    v[j] = t;
+  }
+}
+
+static int ra_build(reduce_alloc* A, const redset_hip_rs* rs, int p, int e, int kind, int missing, const int* lost,
+                    const redset_hip_shard_layout* L, int world) {
+  memset(A, 0, sizeof(*A));
+  A->world = world;
+  A->nsets = L->nsets;
+  A->p = p;
+  A->e = e;
+  A->d = p - e;
+  A->mh = L->max_hosted;
+  A->W = L->slice_bytes;
+  A->C = L->chunk_size;
+  A->host = L->host;
+  A->slot = L->slot;
+  if (world < 2 || world > REDUCE_MAX_WORLD) return 0; /* not ok: nothing to reduce, or too wide */
+  for (int q = 0; q < world; ++q)
+    if ((size_t) q * A->W < A->C) A->nslices = q + 1;
+  if (set_outputs(rs, p, e, kind, missing, lost, &A->oc, &A->coef, &A->nout)) return REDSET_FAILURE;
+  const size_t nk = (size_t) A->nsets * A->nout, nkey = nk * (size_t) world * (size_t) world;
+  if (nkey > ((size_t) 1 << 26)) return 0; /* too many rows to plan this way */
+  A->ord = malloc(sizeof(int) * nk);
+  A->mask = calloc(nk, sizeof(uint64_t));
+  A->srow = malloc(sizeof(long) * nkey);
+  A->rrow = malloc(sizeof(long) * nkey);
+  A->S = calloc((size_t) world, sizeof(long));
+  A->R = calloc((size_t) world, sizeof(long));
+  A->sent = calloc((size_t) world, sizeof(unsigned long long));
+  A->recvd = calloc((size_t) world, sizeof(unsigned long long));
+  if (!A->ord || !A->mask || !A->srow || !A->rrow || !A->S || !A->R || !A->sent || !A->recvd)
+    return sfail("out of host memory");
+  for (size_t i = 0; i < nkey; ++i) A->srow[i] = A->rrow[i] = -1;
+  A->ok = 1;
+  for (int k = 0; k < A->nsets; ++k) {
+    for (int o = 0; o < A->nout; ++o) {
+      uint64_t m = 0;
+      for (int t = 0; t < p; ++t)
+        if (A->coef[(size_t) o * p + t]) m |= (uint64_t) 1 << A->host[(size_t) k * p + t];
+      A->mask[(size_t) k * A->nout + o] = m;
+      if (!m) A->ok = 0; /* an output nothing feeds: not this shape's business */
+      A->ord[(size_t) k * A->nout + o] = o;
+    }
+    ra_sort(A, k, A->ord + (size_t) k * A->nout, A->nout);
+  }
+  /* sender g's rows, in the order (set, receiver, slice, output) */
+  for (int k = 0; k < A->nsets; ++k)
+    for (int h = 0; h < world; ++h)
+      for (int q = 0; q < A->nslices; ++q)
+        for (int i = 0; i < A->nout; ++i) {
+          const int o = A->ord[(size_t) k * A->nout + i];
+          if (ra_host(A, k, o) != h) continue;
+          const uint64_t rem = ra_remote(A, k, o);
+          for (int g = 0; g < world; ++g)
+            if (rem >> g & 1) {
+              A->srow[ra_key(A, k, o, q, g)] = A->S[g]++;
+              ++A->sent[g];
+              ++A->recvd[h];
+            }
+        }
+  /* receiver h's scratch rows (after its sent ones), in the order (set,
+   * sender, slice, output); the first remote contributor's go straight in
+   * the output */
+  for (int k = 0; k < A->nsets; ++k)
+    for (int h = 0; h < world; ++h)
+      for (int g = 0; g < world; ++g)
+        for (int q = 0; q < A->nslices; ++q)
+          for (int i = 0; i < A->nout; ++i) {
+            const int o = A->ord[(size_t) k * A->nout + i];
+            if (ra_host(A, k, o) != h) continue;
+            const uint64_t rem = ra_remote(A, k, o);
+            if (!(rem >> g & 1) || (rem & (~rem + 1)) == ((uint64_t) 1 << g)) continue;
+            A->rrow[ra_key(A, k, o, q, g)] = A->R[h]++;
+          }
+  A->rows = (long) world * A->mh * (A->d + A->e);
+  for (int g = 0; g < world; ++g) {
+    for (int k = 0; k < A->nsets; ++k) /* receiver rows start after the sent ones */
+      for (int o = 0; o < A->nout; ++o)
+        if (ra_host(A, k, o) == g)
+          for (int q = 0; q < A->nslices; ++q)
+            for (int s = 0; s < world; ++s) {
+              long* r = &A->rrow[ra_key(A, k, o, q, s)];
+              if (*r >= 0) *r += A->S[g];
+            }
+    if (A->S[g] + A->R[g] > A->rows) A->ok = 0;
+  }
+  return 0;
+}
+
+/* a row's place in process memory: buffer (0 hosted data, 1 hosted parity,
+ * 2 gathered data, 3 gathered parity) and offset */
+typedef struct {
+  int buf;
+  size_t off;
+} rloc;
+
+static rloc ra_scratch(const reduce_alloc* A, long row) {
+  const long nD = (long) A->world * A->mh * A->d;
+  rloc l = {row < nD ? 2 : 3, (size_t) (row < nD ? row : row - nD) * A->W};
+  return l;
+}
+static rloc ra_output(const reduce_alloc* A, int k, int o, int q) {
+  const ocell* O = &A->oc[o];
+  const int j = ra_slot(A, k, o);
+  rloc l = {O->pass, (((size_t) q * A->mh + (size_t) j) * (size_t) (O->pass ? A->e : A->d) + (size_t) O->x) * A->W};
+  return l;
+}
+/* where sender g's row of (k, o, q) lands at the receiver */
+static rloc ra_dest(const reduce_alloc* A, int k, int o, int q, int g) {
+  const long r = A->rrow[ra_key(A, k, o, q, g)];
+  return r < 0 ? ra_output(A, k, o, q) : ra_scratch(A, r);
+}
+
+static unsigned char* ra_ptr(const redset_hip_shard_layout* L, rloc l) {
+  unsigned char* base[4] = {L->hosted_data, L->hosted_parity, L->gathered_data, L->gathered_parity};
+  return base[l.buf] + l.off;
+}
+
+/* member t of set k's cell in stripe c, slice q, in my hosted slabs */
+static unsigned char* ra_input(const reduce_alloc* A, const redset_hip_shard_layout* L, int kind, int k, int t, int c,
+                               int q) {
+  const int j = A->slot[(size_t) k * A->p + t], x = cell_of(A->p, A->e, kind, t, c);
+  rloc l = {x >= 0 ? 0 : 1, 0};
+  l.off = (((size_t) q * A->mh + (size_t) j) * (size_t) (x >= 0 ? A->d : A->e) + (size_t) (x >= 0 ? x : -(1 + x))) * A->W;
+  return ra_ptr(L, l);
+}
+
+/* one direction of a pair's rows in set k as merged messages: the rows of
+ * outputs hosted by `h` that `g` contributes to, (slice, output) order;
+ * g == me: my sends to h, else my receives from g (h == me) */
+static int ra_messages(const reduce_alloc* A, const redset_hip_shard_layout* L, int k, int g, int h, int me,
+                       xlist* out, int* nmsg, unsigned long long* bytes) {
+  int have = 0;
+  rloc s0 = {0, 0}, r0 = {0, 0};
+  size_t len = 0;
+  for (int q = 0; q < A->nslices; ++q)
+    for (int i = 0; i < A->nout; ++i) {
+      const int o = A->ord[(size_t) k * A->nout + i];
+      if (ra_host(A, k, o) != h || !(ra_remote(A, k, o) >> g & 1)) continue;
+      const rloc sl = ra_scratch(A, A->srow[ra_key(A, k, o, q, g)]), rl = ra_dest(A, k, o, q, g);
+      if (have && sl.buf == s0.buf && sl.off == s0.off + len && rl.buf == r0.buf && rl.off == r0.off + len) {
+        len += A->W;
+        continue;
+      }
+      if (have) {
+        redset_hip_xfer x = {g == me ? h : g, g == me, ra_ptr(L, g == me ? s0 : r0), len};
+        if (xl_push(out, x)) return REDSET_FAILURE;
+        ++*nmsg;
+        *bytes += len;
+      }
+      have = 1;
+      s0 = sl;
+      r0 = rl;
+      len = A->W;
+    }
+  if (have) {
+    redset_hip_xfer x = {g == me ? h : g, g == me, ra_ptr(L, g == me ? s0 : r0), len};
+    if (xl_push(out, x)) return REDSET_FAILURE;
+    ++*nmsg;
+    *bytes += len;
+  }
+  return 0;
+}
+
+/* my combines and exchanges of the partial-sum shape (A->ok) */
+static int plan_reduce(redset_hip_sharded* P, const reduce_alloc* A, const redset_hip_shard_layout* L, int kind,
+                       int me) {
+  const int world = A->world, p = A->p, nout = A->nout;
+  int rc = 0;
+  P->part = calloc((size_t) A->nsets, sizeof(cset));
+  P->acc = calloc((size_t) A->nsets, sizeof(cset));
+  P->goff = calloc((size_t) A->nsets + 1, sizeof(int));
+  P->roff = calloc((size_t) A->nsets + 1, sizeof(int));
+  int* sel = malloc(sizeof(int) * (size_t) nout);
+  int* ins = malloc(sizeof(int) * (size_t) p);
+  const size_t maxin = (size_t) p + (size_t) nout * (size_t) world;
+  unsigned char** ip = malloc(sizeof(*ip) * maxin);
+  unsigned char** op = malloc(sizeof(*op) * (size_t) nout);
+  unsigned char* cf = malloc(maxin * (size_t) nout);
+  if (!P->part || !P->acc || !P->goff || !P->roff || !sel || !ins || !ip || !op || !cf) rc = sfail("out of host memory");
+  for (int k = 0; k < A->nsets && !rc; ++k) {
+    /* combines: stripe by stripe, slice by slice, the outputs grouped by host */
+    for (int c = 0; c < p && !rc; ++c)
+      for (int q = 0; q < A->nslices && !rc; ++q) {
+        const size_t n = A->C - (size_t) q * A->W < A->W ? A->C - (size_t) q * A->W : A->W;
+        for (int h = 0; h < world && !rc; ++h)
+          for (int grp = 0; grp < (h == me ? 2 : 1) && !rc; ++grp) {
+            /* grp 0: partials for h (or, h == me, outputs only my inputs
+             * feed: COMPUTE); grp 1: my outputs partials arrive for
+             * (ACCUMULATE) */
+            int ns = 0;
+            for (int o = 0; o < nout; ++o) {
+              if (A->oc[o].c != c || ra_host(A, k, o) != h) continue;
+              const uint64_t rem = ra_remote(A, k, o);
+              if (h != me ? (rem >> me & 1) : (grp == 0 ? rem == 0 : rem != 0)) sel[ns++] = o;
+            }
+            if (ns == 0) continue;
+            /* my inputs with a coefficient for one of them */
+            int ni = 0;
+            for (int t = 0; t < p; ++t) {
+              if (A->host[(size_t) k * p + t] != me) continue;
+              int used = 0;
+              for (int a = 0; a < ns && !used; ++a) used = A->coef[(size_t) sel[a] * p + t] != 0;
+              if (used) ins[ni++] = t;
+            }
+            int nin = ni;
+            for (int a = 0; a < ni; ++a) ip[a] = ra_input(A, L, kind, k, ins[a], c, q);
+            /* the accumulate's extra inputs: partials in my scratch */
+            const int extra0 = nin;
+            for (int a = 0; grp == 1 && a < ns; ++a)
+              for (int g = 0; g < world; ++g) {
+                const long r = A->rrow[ra_key(A, k, sel[a], q, g)];
+                if (ra_remote(A, k, sel[a]) >> g & 1 && r >= 0) ip[nin++] = ra_ptr(L, ra_scratch(A, r));
+              }
+            if (nin == 0) {
+              if (grp == 0 && h == me) rc = sfail("sharded plan: an output with no input");
+              continue; /* grp 1: the one partial that arrived is the output */
+            }
+            memset(cf, 0, (size_t) nin * (size_t) ns);
+            int ex = extra0;
+            for (int a = 0; a < ns; ++a) {
+              const int o = sel[a];
+              for (int b = 0; b < ni; ++b) cf[(size_t) a * nin + b] = A->coef[(size_t) o * p + ins[b]];
+              op[a] = h == me ? ra_ptr(L, ra_output(A, k, o, q)) : ra_ptr(L, ra_scratch(A, A->srow[ra_key(A, k, o, q, me)]));
+              for (int g = 0; grp == 1 && g < world; ++g)
+                if (ra_remote(A, k, o) >> g & 1 && A->rrow[ra_key(A, k, o, q, g)] >= 0) cf[(size_t) a * nin + ex++] = 1;
+            }
+            rc = cs_add(grp == 1 ? &P->acc[k] : &P->part[k], nin, ip, ns, op, cf, grp == 1, n);
+          }
+      }
+    /* the partial exchange: per peer my sends, then my receives */
+    xlist X;
+    memset(&X, 0, sizeof(X));
+    for (int g = 0; g < world && !rc; ++g) {
+      if (g == me) continue;
+      rc = ra_messages(A, L, k, me, g, me, &X, &P->info.return_messages, &P->info.return_bytes_sent);
+      if (!rc) rc = ra_messages(A, L, k, g, me, me, &X, &P->info.return_recv_messages, &P->info.return_bytes_recv);
+    }
+    for (int i = 0; i < X.n && !rc; ++i) {
+      if (X.v[i].send) {
+        if (X.v[i].len > P->info.return_msg_max) P->info.return_msg_max = X.v[i].len;
+        if (!P->info.return_msg_min || X.v[i].len < P->info.return_msg_min) P->info.return_msg_min = X.v[i].len;
+      }
+      rc = xl_push(&P->ret, X.v[i]);
+    }
+    free(X.v);
+    P->goff[k + 1] = 0;
+    P->roff[k + 1] = P->ret.n;
+    cs_finish(&P->part[k]);
+    cs_finish(&P->acc[k]);
+    P->info.compute_bytes += P->part[k].bytes + P->acc[k].bytes;
+  }
+  free(sel);
+  free(ins);
+  free(ip);
+  free(op);
+  free(cf);
+  return rc;
+}
+
+/* the gather shape's bytes sent / received by process `who` (the planner's
+ * own lists, merged as it merges them) */
+static int gather_counts(const pctx* C0, int who, unsigned long long* sent, unsigned long long* recvd) {
+  pctx C = *C0;
+  C.me = who;
+  C.me_s = C.sidx[who];
+  *sent = *recvd = 0;
+  int rc = 0;
+  for (int k = 0; k < C.L->nsets && !rc; ++k) {
+    exch G, R;
+    rc = ex_init(&G, C.world, who);
+    if (!rc) rc = ex_init(&R, C.world, who);
+    if (!rc) rc = plan_gather(&C, k, &G);
+    if (!rc) rc = plan_return(&C, k, &R);
+    for (int g = 0; g < C.world && !rc; ++g) {
+      for (int i = 0; i < G.send[g].n; ++i) *sent += G.send[g].v[i].len;
+      for (int i = 0; i < R.send[g].n; ++i) *sent += R.send[g].v[i].len;
+      for (int i = 0; i < G.recv[g].n; ++i) *recvd += G.recv[g].v[i].len;
+      for (int i = 0; i < R.recv[g].n; ++i) *recvd += R.recv[g].v[i].len;
+    }
+    ex_free(&G);
+    ex_free(&R);
+  }
+  return rc;
+}
+
+/* what the _ex entry points pass down; the legacy ones plan GATHER and
+ * compare nothing */
+typedef struct {
+  int shape;       /* REDSET_HIP_SHAPE_* */
+  int compare;     /* count both shapes (the _ex entry points) */
+  int (*combine)(void*, const redset_hip_combine_job*, int, size_t, void*);
+  void* combine_ctx;
+} shape_req;
+
 /* the plan of either scheme: rs (RS kinds) or NULL (XOR kinds, e = 1);
  * compute: which processes compute a column slice (NULL: all) */
 static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missing, const int* rebuild_ranks,
                      const redset_hip_shard_layout* L, const int* compute, const redset_hip_transport* tr,
-                     const redset_hip_compute* comp, redset_hip_sharded** out) {
+                     const redset_hip_compute* comp, const shape_req* want, redset_hip_sharded** out) {
   if (is_encode(kind)) missing = 0;
   if (!is_encode(kind)) {
     if (missing < 1 || missing > e) return sfail("cannot rebuild %d members with %d parity chunks", missing, e);
@@ -355,8 +881,10 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
   unsigned char* need = malloc((size_t) p * p);
   int* by_slot = malloc(sizeof(int) * (size_t) world * mh); /* (h, j) -> member, or -1 */
   exch G, R;
+  reduce_alloc A;
   memset(&G, 0, sizeof(G));
   memset(&R, 0, sizeof(R));
+  memset(&A, 0, sizeof(A));
   int rc = (!P || !need || !by_slot) ? sfail("out of host memory") : 0;
   if (!rc) rc = ex_init(&G, world, me);
   if (!rc) rc = ex_init(&R, world, me);
@@ -373,6 +901,9 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
   P->info.rank = me;
   P->info.nsets = L->nsets;
   P->info.missing = missing;
+  P->shape = REDSET_HIP_SHAPE_GATHER;
+  P->shape_info.struct_size = sizeof(P->shape_info);
+  P->shape_info.scratch_bytes = (unsigned long long) world * mh * p * W;
   if (sidx[me] >= 0) {
     const size_t lo = (size_t) sidx[me] * W;
     P->info.my_slice_len = lo >= L->chunk_size ? 0 : (L->chunk_size - lo < W ? L->chunk_size - lo : W);
@@ -382,6 +913,64 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
   if ((rc = plan_inputs(rs, p, e, kind, missing, rebuild_ranks, need))) goto done;
 
   pctx C = {L, by_slot, need, p, e, d, mh, world, me, kind, missing, P->lost, W, sidx, sidx[me]};
+
+  /* the shape: both counted (the _ex entry points), the one asked for or
+   * the one whose busiest process moves fewer bytes */
+  if (want && want->compare) {
+    redset_hip_sharded_shape_info* S = &P->shape_info;
+    for (int g = 0; g < world && !rc; ++g) {
+      if (world > REDUCE_MAX_WORLD && g != me) continue; /* wide worlds: my own counts only */
+      unsigned long long sn = 0, rv = 0;
+      rc = gather_counts(&C, g, &sn, &rv);
+      const unsigned long long b = sn > rv ? sn : rv;
+      if (b > S->gather_busiest_bytes) S->gather_busiest_bytes = b;
+      if (g == me) S->gather_bytes_sent = sn, S->gather_bytes_recv = rv;
+    }
+    /* the partial sums need every process computing, and either the HIP
+     * plans or a combine callback (a whole-set callback cannot run them) */
+    const int can = !compute && (!comp || !comp->run || want->combine);
+    if (!rc && can) rc = ra_build(&A, rs, p, e, kind, missing, rebuild_ranks, L, world);
+    if (!rc && A.ok) {
+      S->reduce_possible = 1;
+      for (int g = 0; g < world; ++g) {
+        const unsigned long long b = (A.sent[g] > A.recvd[g] ? A.sent[g] : A.recvd[g]) * W;
+        if (b > S->reduce_busiest_bytes) S->reduce_busiest_bytes = b;
+      }
+      S->reduce_bytes_sent = A.sent[me] * W;
+      S->reduce_bytes_recv = A.recvd[me] * W;
+      S->scratch_bytes_needed = (unsigned long long) (A.S[me] + A.R[me]) * W;
+    }
+    if (!rc && want->shape == REDSET_HIP_SHAPE_REDUCE && !A.ok)
+      rc = sfail(world < 2 ? "sharded plan: the partial-sum shape needs at least 2 processes"
+                 : !can   ? "sharded plan: the partial-sum shape needs every process computing and HIP or combine compute"
+                          : "sharded plan: the partial sums do not fit the gathered slabs (or over 64 processes)");
+    if (!rc && A.ok &&
+        (want->shape == REDSET_HIP_SHAPE_REDUCE ||
+         (want->shape == REDSET_HIP_SHAPE_AUTO && S->reduce_busiest_bytes < S->gather_busiest_bytes)))
+      P->shape = REDSET_HIP_SHAPE_REDUCE;
+  }
+  P->shape_info.shape = P->shape;
+  if (rc) goto done;
+
+  if (P->shape == REDSET_HIP_SHAPE_REDUCE) {
+    P->combine = want->combine;
+    P->combine_ctx = want->combine_ctx;
+    P->info.my_slice_len = L->chunk_size; /* every process combines whole cells' worth of its inputs */
+    rc = plan_reduce(P, &A, L, kind, me);
+    P->shape_info.reduce_messages = P->info.return_messages;
+    P->shape_info.reduce_recv_messages = P->info.return_recv_messages;
+    if (!rc && !P->combine) {
+      P->part_plans = calloc((size_t) L->nsets, sizeof(*P->part_plans));
+      P->acc_plans = calloc((size_t) L->nsets, sizeof(*P->acc_plans));
+      if (!P->part_plans || !P->acc_plans) rc = sfail("out of host memory");
+      for (int k = 0; k < L->nsets && !rc; ++k) {
+        if (P->part[k].n) rc = redset_hip_plan_combine(P->part[k].v, P->part[k].n, W, &P->part_plans[k]);
+        if (!rc && P->acc[k].n) rc = redset_hip_plan_combine(P->acc[k].v, P->acc[k].n, W, &P->acc_plans[k]);
+      }
+    }
+    goto done;
+  }
+
   P->goff = calloc((size_t) L->nsets + 1, sizeof(int));
   P->roff = calloc((size_t) L->nsets + 1, sizeof(int));
   if (!P->goff || !P->roff) {
@@ -440,6 +1029,7 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
 done:
   ex_free(&G);
   ex_free(&R);
+  ra_free(&A);
   free(need);
   free(by_slot);
   free(sidx);
@@ -462,7 +1052,7 @@ int redset_hip_rs_sharded_plan_on(const redset_hip_rs* rs, int kind, int missing
   if (redset_hip_rs_shape(rs, &p, &e)) return REDSET_FAILURE;
   if (kind != REDSET_HIP_PLAN_RS_ENCODE && kind != REDSET_HIP_PLAN_RS_REBUILD)
     return sfail("sharded_plan: kind %d is not RS encode or rebuild", kind);
-  return plan_sets(rs, p, e, kind, missing, rebuild_ranks, L, compute, tr, comp, out);
+  return plan_sets(rs, p, e, kind, missing, rebuild_ranks, L, compute, tr, comp, NULL, out);
 }
 
 int redset_hip_rs_sharded_plan(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
@@ -483,13 +1073,66 @@ int redset_hip_xor_sharded_plan_on(int ranks, int kind, int root, const redset_h
   if (kind == REDSET_HIP_PLAN_XOR_REBUILD && (root < 0 || root >= ranks))
     return sfail("root %d out of range", root);
   return plan_sets(NULL, ranks, 1, kind, kind == REDSET_HIP_PLAN_XOR_REBUILD ? 1 : 0, &root, L, compute, tr, comp,
-                   out);
+                   NULL, out);
 }
 
 int redset_hip_xor_sharded_plan(int ranks, int kind, int root, const redset_hip_shard_layout* L,
                                 const redset_hip_transport* tr, const redset_hip_compute* comp,
                                 redset_hip_sharded** out) {
   return redset_hip_xor_sharded_plan_on(ranks, kind, root, L, NULL, tr, comp, out);
+}
+
+static int opts_req(const redset_hip_sharded_opts* o, shape_req* w) {
+  memset(w, 0, sizeof(*w));
+  w->compare = 1;
+  if (!o) return 0;
+  if (o->struct_size != sizeof(*o))
+    return sfail("sharded_plan_ex: opts.struct_size %zu, this library's is %zu", o->struct_size, sizeof(*o));
+  if (o->shape < REDSET_HIP_SHAPE_AUTO || o->shape > REDSET_HIP_SHAPE_REDUCE)
+    return sfail("sharded_plan_ex: unknown shape %d", o->shape);
+  w->shape = o->shape;
+  w->combine = o->combine;
+  w->combine_ctx = o->combine_ctx;
+  return 0;
+}
+
+int redset_hip_rs_sharded_plan_ex(const redset_hip_rs* rs, int kind, int missing, const int* rebuild_ranks,
+                                  const redset_hip_shard_layout* L, const redset_hip_transport* tr,
+                                  const redset_hip_sharded_opts* opts, redset_hip_sharded** out) {
+  int p, e;
+  shape_req w;
+  if (!out) return sfail("sharded_plan_ex: null out-pointer");
+  *out = NULL;
+  if (!rs || !L || !tr || !tr->exchange) return sfail("sharded_plan_ex: null argument");
+  if (opts_req(opts, &w)) return REDSET_FAILURE;
+  if (redset_hip_rs_shape(rs, &p, &e)) return REDSET_FAILURE;
+  if (kind != REDSET_HIP_PLAN_RS_ENCODE && kind != REDSET_HIP_PLAN_RS_REBUILD)
+    return sfail("sharded_plan_ex: kind %d is not RS encode or rebuild", kind);
+  return plan_sets(rs, p, e, kind, missing, rebuild_ranks, L, opts ? opts->compute_on : NULL, tr,
+                   opts ? opts->compute : NULL, &w, out);
+}
+
+int redset_hip_xor_sharded_plan_ex(int ranks, int kind, int root, const redset_hip_shard_layout* L,
+                                   const redset_hip_transport* tr, const redset_hip_sharded_opts* opts,
+                                   redset_hip_sharded** out) {
+  shape_req w;
+  if (!out) return sfail("xor_sharded_plan_ex: null out-pointer");
+  *out = NULL;
+  if (!L || !tr || !tr->exchange) return sfail("xor_sharded_plan_ex: null argument");
+  if (opts_req(opts, &w)) return REDSET_FAILURE;
+  if (ranks < 2 || ranks > MAX_RANKS) return sfail("XOR needs 2..%d ranks, got %d", MAX_RANKS, ranks);
+  if (kind != REDSET_HIP_PLAN_XOR_ENCODE && kind != REDSET_HIP_PLAN_XOR_REBUILD)
+    return sfail("xor_sharded_plan_ex: kind %d is not XOR encode or rebuild", kind);
+  if (kind == REDSET_HIP_PLAN_XOR_REBUILD && (root < 0 || root >= ranks))
+    return sfail("root %d out of range", root);
+  return plan_sets(NULL, ranks, 1, kind, kind == REDSET_HIP_PLAN_XOR_REBUILD ? 1 : 0, &root, L,
+                   opts ? opts->compute_on : NULL, tr, opts ? opts->compute : NULL, &w, out);
+}
+
+int redset_hip_sharded_get_shape(const redset_hip_sharded* P, redset_hip_sharded_shape_info* info, size_t size) {
+  if (!P || !info) return sfail("null argument");
+  memcpy(info, &P->shape_info, size < sizeof(P->shape_info) ? size : sizeof(P->shape_info));
+  return REDSET_SUCCESS;
 }
 
 static int compute_set(redset_hip_sharded* P, int k, void* stream) {
@@ -511,17 +1154,35 @@ static int exchange(redset_hip_sharded* P, const xlist* L, int lo, int hi, void*
   return REDSET_SUCCESS;
 }
 
+/* the partial-sum shape's combines of set k: COMPUTE (partials, outputs
+ * only my inputs feed) or ACCUMULATE (outputs partials arrived for) */
+static int reduce_set(redset_hip_sharded* P, int k, int acc, void* stream) {
+  const cset* S = acc ? &P->acc[k] : &P->part[k];
+  if (S->n == 0) return REDSET_SUCCESS;
+  if (P->combine) {
+    if (P->combine(P->combine_ctx, S->v, S->n, P->W, stream) != 0)
+      return sfail("sharded combine callback failed (set %d)", k);
+    return REDSET_SUCCESS;
+  }
+  return redset_hip_plan_execute(acc ? P->acc_plans[k] : P->part_plans[k], stream);
+}
+
 int redset_hip_sharded_execute_phase(redset_hip_sharded* P, int phase, void* stream) {
   if (!P) return sfail("null sharded plan");
+  const int reduce = P->shape == REDSET_HIP_SHAPE_REDUCE;
   switch (phase) {
     case REDSET_HIP_PHASE_GATHER:
-      return exchange(P, &P->gather, 0, P->gather.n, stream, "gather");
+      return reduce ? REDSET_SUCCESS : exchange(P, &P->gather, 0, P->gather.n, stream, "gather");
     case REDSET_HIP_PHASE_COMPUTE:
       for (int k = 0; k < P->info.nsets; ++k)
-        if (compute_set(P, k, stream)) return REDSET_FAILURE;
+        if (reduce ? reduce_set(P, k, 0, stream) : compute_set(P, k, stream)) return REDSET_FAILURE;
       return REDSET_SUCCESS;
     case REDSET_HIP_PHASE_RETURN:
-      return exchange(P, &P->ret, 0, P->ret.n, stream, "return");
+      return exchange(P, &P->ret, 0, P->ret.n, stream, reduce ? "partial sums" : "return");
+    case REDSET_HIP_PHASE_ACCUMULATE:
+      for (int k = 0; k < P->info.nsets && reduce; ++k)
+        if (reduce_set(P, k, 1, stream)) return REDSET_FAILURE;
+      return REDSET_SUCCESS;
     default:
       return sfail("unknown sharded phase %d", phase);
   }
@@ -541,6 +1202,61 @@ static int hfail(const char* what, hipError_t e) { return sfail("sharded execute
  * members are in them and would wait forever, src/redset_reedsolomon.c:
  * 338-342): the bytes this member sends are then unspecified, and the error
  * is returned at the end. */
+/* the plan's exchange stream and events, made on the first execute */
+static int pipe_setup(redset_hip_sharded* P) {
+  hipError_t e;
+  int rc = 0;
+  const int n = P->info.nsets;
+  if (!P->xstream && !P->ev_c) {
+    P->ev_c = calloc((size_t) n, sizeof(hipEvent_t));
+    P->ev_r = calloc((size_t) n, sizeof(hipEvent_t));
+    if (!P->ev_c || !P->ev_r) rc = sfail("out of host memory");
+    if (!rc && (e = hipStreamCreateWithFlags(&P->xstream, hipStreamNonBlocking)) != hipSuccess) rc = hfail("stream", e);
+    if (!rc && (e = hipEventCreateWithFlags(&P->ev_x, hipEventDisableTiming)) != hipSuccess) rc = hfail("event", e);
+    for (int k = 0; k < n && !rc; ++k)
+      if ((e = hipEventCreateWithFlags(&P->ev_c[k], hipEventDisableTiming)) != hipSuccess ||
+          (e = hipEventCreateWithFlags(&P->ev_r[k], hipEventDisableTiming)) != hipSuccess)
+        rc = hfail("event", e);
+  } else if (!P->xstream || !P->ev_x) {
+    rc = sfail("sharded execute: the plan's stream or events were not created");
+  }
+  return rc;
+}
+
+/* The partial-sum shape pipelined: every set's partial sums on the caller's
+ * stream, one after another; set k's exchange on the exchange stream as soon
+ * as its partials are made (so it overlaps set k+1's); set k's accumulate on
+ * the caller's stream once its exchange is done. Host order: all partial
+ * combines enqueued first, then per set its exchange and accumulate, so a
+ * transport that completes its exchange before returning (MPI) overlaps the
+ * same way. Every exchange runs after a local error (the peers are in it). */
+static int execute_reduce(redset_hip_sharded* P, hipStream_t s) {
+  hipError_t e;
+  const int n = P->info.nsets;
+  if (P->ret.n == 0) {
+    int rc = 0;
+    for (int k = 0; k < n && !rc; ++k) rc = reduce_set(P, k, 0, s);
+    for (int k = 0; k < n && !rc; ++k) rc = reduce_set(P, k, 1, s);
+    return rc;
+  }
+  int rc = pipe_setup(P);
+  hipStream_t x = P->xstream ? P->xstream : s;
+  if (!rc && ((e = hipEventRecord(P->ev_x, s)) != hipSuccess || (e = hipStreamWaitEvent(x, P->ev_x, 0)) != hipSuccess))
+    rc = hfail("order after the caller's stream", e);
+  for (int k = 0; k < n; ++k) {
+    if (!rc && reduce_set(P, k, 0, s)) rc = REDSET_FAILURE;
+    if (!rc && (e = hipEventRecord(P->ev_c[k], s)) != hipSuccess) rc = hfail("partials event", e);
+  }
+  for (int k = 0; k < n; ++k) {
+    if (!rc && (e = hipStreamWaitEvent(x, P->ev_c[k], 0)) != hipSuccess) rc = hfail("partials -> exchange", e);
+    if (exchange(P, &P->ret, P->roff[k], P->roff[k + 1], x, "partial sums") && !rc) rc = REDSET_FAILURE;
+    if (!rc && ((e = hipEventRecord(P->ev_r[k], x)) != hipSuccess || (e = hipStreamWaitEvent(s, P->ev_r[k], 0)) != hipSuccess))
+      rc = hfail("exchange -> accumulate", e);
+    if (!rc && reduce_set(P, k, 1, s)) rc = REDSET_FAILURE;
+  }
+  return rc;
+}
+
 static int execute_pipelined(redset_hip_sharded* P, hipStream_t s) {
   hipError_t e;
   int rc = 0;
@@ -552,16 +1268,7 @@ static int execute_pipelined(redset_hip_sharded* P, hipStream_t s) {
     for (int k = 0; k < n && !rc; ++k) rc = compute_set(P, k, s);
     return rc;
   }
-  if (!P->xstream && !P->ev_c) {
-    P->ev_c = calloc((size_t) n, sizeof(hipEvent_t));
-    if (!P->ev_c) rc = sfail("out of host memory");
-    if (!rc && (e = hipStreamCreateWithFlags(&P->xstream, hipStreamNonBlocking)) != hipSuccess) rc = hfail("stream", e);
-    if (!rc && (e = hipEventCreateWithFlags(&P->ev_x, hipEventDisableTiming)) != hipSuccess) rc = hfail("event", e);
-    for (int k = 0; k < n && !rc; ++k)
-      if ((e = hipEventCreateWithFlags(&P->ev_c[k], hipEventDisableTiming)) != hipSuccess) rc = hfail("event", e);
-  } else if (!P->xstream || !P->ev_x) {
-    rc = sfail("sharded execute: the plan's stream or events were not created");
-  }
+  rc = pipe_setup(P);
   /* without its own stream (a failed setup) the exchanges go on `s` */
   hipStream_t x = P->xstream ? P->xstream : s;
   /* the exchange stream starts after the caller's work (ev_c[0] is free until
@@ -587,14 +1294,15 @@ static int execute_pipelined(redset_hip_sharded* P, hipStream_t s) {
 
 int redset_hip_sharded_execute(redset_hip_sharded* P, void* stream) {
   if (!P) return sfail("null sharded plan");
-  if (P->comp.run) {
+  const int reduce = P->shape == REDSET_HIP_SHAPE_REDUCE;
+  if ((!reduce && P->comp.run) || (reduce && P->combine)) {
     /* every phase runs after a failed one (see execute_pipelined) */
     int rc = 0;
-    for (int ph = REDSET_HIP_PHASE_GATHER; ph <= REDSET_HIP_PHASE_RETURN; ++ph)
+    for (int ph = REDSET_HIP_PHASE_GATHER; ph <= REDSET_HIP_PHASE_ACCUMULATE; ++ph)
       if (redset_hip_sharded_execute_phase(P, ph, stream) && !rc) rc = REDSET_FAILURE;
     return rc;
   }
-  return execute_pipelined(P, (hipStream_t) stream);
+  return reduce ? execute_reduce(P, (hipStream_t) stream) : execute_pipelined(P, (hipStream_t) stream);
 }
 
 int redset_hip_sharded_get_info(const redset_hip_sharded* P, redset_hip_sharded_info* info) {
@@ -607,10 +1315,23 @@ void redset_hip_sharded_destroy(redset_hip_sharded* P) {
   if (!P) return;
   for (int k = 0; P->plans && k < P->info.nsets; ++k) redset_hip_plan_destroy(P->plans[k]);
   free(P->plans);
+  for (int k = 0; k < P->info.nsets; ++k) {
+    if (P->part_plans) redset_hip_plan_destroy(P->part_plans[k]);
+    if (P->acc_plans) redset_hip_plan_destroy(P->acc_plans[k]);
+    if (P->part) cs_free(&P->part[k]);
+    if (P->acc) cs_free(&P->acc[k]);
+  }
+  free(P->part_plans);
+  free(P->acc_plans);
+  free(P->part);
+  free(P->acc);
   if (P->xstream) (void) hipStreamSynchronize(P->xstream);
   for (int k = 0; P->ev_c && k < P->info.nsets; ++k)
     if (P->ev_c[k]) (void) hipEventDestroy(P->ev_c[k]);
+  for (int k = 0; P->ev_r && k < P->info.nsets; ++k)
+    if (P->ev_r[k]) (void) hipEventDestroy(P->ev_r[k]);
   free(P->ev_c);
+  free(P->ev_r);
   if (P->ev_x) (void) hipEventDestroy(P->ev_x);
   if (P->xstream) (void) hipStreamDestroy(P->xstream);
   free(P->goff);

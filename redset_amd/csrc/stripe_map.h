@@ -31,6 +31,7 @@ struct StripeMap {
   std::vector<CellRef> out;
   std::vector<uint8_t> coef;
   bool xor_only = false;  // XOR scheme: every coefficient is 1
+  bool accumulate = false;  // XOR into the outputs (redset_hip_plan_combine jobs)
 };
 
 // cell of member `rank` in RS stripe `chunk` (src/redset_reedsolomon_common.c:822-853)

@@ -39,6 +39,13 @@ static pthread_once_t rccl_once = PTHREAD_ONCE_INIT;
 static void rccl_open(void) {
   static const char* names[] = {"librccl.so.1", "librccl.so", "/opt/rocm/lib/librccl.so.1", "/opt/rocm/lib/librccl.so"};
   void* h = NULL;
+#if REDSET_HIP_TEST_KNOBS
+  /* test builds: a stand-in RCCL by path (tests/rcclstub), for processes
+   * where the real librccl.so.1 is already mapped (torch's) and a library
+   * search would return it */
+  const char* stub = getenv("REDSET_HIP_TEST_RCCL_LIBRARY");
+  if (stub && stub[0]) h = dlopen(stub, RTLD_NOW | RTLD_LOCAL);
+#endif
   for (size_t i = 0; i < sizeof(names) / sizeof(names[0]) && !h; ++i) h = dlopen(names[i], RTLD_NOW | RTLD_LOCAL);
   if (!h) {
     snprintf(rccl.err, sizeof(rccl.err), "RCCL transport: cannot load librccl (%s)", dlerror());

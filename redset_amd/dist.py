@@ -149,12 +149,35 @@ class RcclTransport:
 class CallbackCompute:
     """redset_hip_compute over a Python backend with
     ``run(kind, lost, lofi_views, parity_views, nbytes, stride)`` (tests put
-    the CPU oracle here)."""
+    the CPU oracle here), and, if the backend has
+    ``combine(jobs, nbytes, bufs)`` with jobs as (input addresses, output
+    addresses, nout x nin coefficients, accumulate), the partial-sum shape's
+    combine callback too."""
 
     def __init__(self, backend, p: int, bufs: _Buffers):
         self.backend, self.p, self.bufs = backend, p, bufs
         self._fn = _lib.COMPUTE_FN(self._run)
         self.struct = _lib.Compute(ctypes.cast(self._fn, c_void_p), None)
+        self._cfn = _lib.COMBINE_FN(self._combine) if hasattr(backend, "combine") else None
+
+    @property
+    def combine_ptr(self):
+        return ctypes.cast(self._cfn, c_void_p) if self._cfn is not None else None
+
+    def _combine(self, ctx, jobs, njobs, nbytes, stream) -> int:
+        try:
+            lst = []
+            for k in range(njobs):
+                J = jobs[k]
+                ins = [J.inp[i] for i in range(J.nin)]
+                outs = [J.out[j] for j in range(J.nout)]
+                coef = np.ctypeslib.as_array(J.coef, shape=(J.nout * J.nin,)).reshape(J.nout, J.nin).copy()
+                lst.append((ins, outs, coef, bool(J.accumulate)))
+            self.backend.combine(lst, nbytes, self.bufs)
+            return 0
+        except Exception as exc:  # noqa: BLE001
+            _lib.load().redset_hip_record_error(f"combine callback: {exc}".encode())
+            return 1
 
     def _run(self, ctx, kind, missing, ranks, lofi, parity, nbytes, stride, stream) -> int:
         try:
@@ -175,11 +198,19 @@ class ShardedSetRunner:
 
     def __init__(self, p: int, e: int, chunk: int, lost: Sequence[int], world: int, rank: int,
                  device=None, backend=None, seed: int = 1234, fill: bool = True, transport: Optional[str] = None,
-                 parity_gap: Optional[int] = 0, sets: Optional[int] = None):
+                 parity_gap: Optional[int] = 0, sets: Optional[int] = None, shape: str = "auto"):
         self.p, self.e, self.d = p, e, p - e
         self.chunk, self.world, self.rank = chunk, world, rank
         self.nsets = world if sets is None else sets
         self.lost = sorted(lost)
+        # the exchange's shape (include/redset_hip.h REDSET_HIP_SHAPE_*):
+        # "auto" lets the planner take whichever moves fewer bytes through
+        # the busiest GPU -- gathering column slices of the inputs, or
+        # sending partial sums of each GPU's own inputs to the outputs' hosts
+        # (one name for both plans, or an (encode, rebuild) pair)
+        names = {"auto": _lib.SHAPE_AUTO, "gather": _lib.SHAPE_GATHER, "reduce": _lib.SHAPE_REDUCE}
+        enc_s, reb_s = (shape, shape) if isinstance(shape, str) else shape
+        self.shape_req = {_lib.PLAN_RS_ENCODE: names[enc_s], _lib.PLAN_RS_REBUILD: names[reb_s]}
         self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
         L = _lib.load()
         self.W = int(L.redset_hip_shard_slice_bytes(chunk, world))
@@ -240,16 +271,29 @@ class ShardedSetRunner:
         L = _lib.load()
         arr = (c_int * max(1, len(lost)))(*lost)
         h = c_void_p()
-        comp = ctypes.byref(self._compute.struct) if self._compute is not None else None
-        _lib.check(L.redset_hip_rs_sharded_plan(self._codec_h, kind, len(lost), arr, ctypes.byref(self._layout),
-                                                ctypes.byref(self._transport.struct), comp, ctypes.byref(h)),
-                   "rs_sharded_plan")
+        opts = _lib.ShardedOpts()
+        opts.struct_size = ctypes.sizeof(_lib.ShardedOpts)
+        opts.shape = self.shape_req[kind]
+        if self._compute is not None:
+            opts.compute = ctypes.pointer(self._compute.struct)
+            opts.combine = self._compute.combine_ptr
+        _lib.check(L.redset_hip_rs_sharded_plan_ex(self._codec_h, kind, len(lost), arr, ctypes.byref(self._layout),
+                                                   ctypes.byref(self._transport.struct), ctypes.byref(opts),
+                                                   ctypes.byref(h)),
+                   "rs_sharded_plan_ex")
         return h
 
     def info(self, op: str) -> dict:
         inf = _lib.ShardedInfo()
         _lib.check(_lib.load().redset_hip_sharded_get_info(self._plans[op], ctypes.byref(inf)), "sharded_get_info")
         return inf.as_dict()
+
+    def shape(self, op: str) -> dict:
+        """The planned shape and both shapes' byte counts (redset_hip_sharded_get_shape)."""
+        si = _lib.ShapeInfo()
+        _lib.check(_lib.load().redset_hip_sharded_get_shape(self._plans[op], ctypes.byref(si), ctypes.sizeof(si)),
+                   "sharded_get_shape")
+        return si.as_dict()
 
     def close(self):
         L = _lib.load()
@@ -292,7 +336,7 @@ class ShardedSetRunner:
     def _run(self, op: str) -> None:
         """One execute: pipelined over the sets (redset_hip_sharded_execute:
         set k+1's gather overlaps set k's gf_mac), or, with ``self.phased``,
-        the three phases one after another with events between them so
+        the four phases one after another with events between them so
         phase_ms() can split the time."""
         L = _lib.load()
         h = self._plans[op]
@@ -307,13 +351,15 @@ class ShardedSetRunner:
         _lib.check(L.redset_hip_sharded_execute_phase(h, _lib.PHASE_COMPUTE, stream), f"sharded {op} compute")
         self._mark(f"{op}_computed")
         _lib.check(L.redset_hip_sharded_execute_phase(h, _lib.PHASE_RETURN, stream), f"sharded {op} return")
+        self._mark(f"{op}_returned")
+        _lib.check(L.redset_hip_sharded_execute_phase(h, _lib.PHASE_ACCUMULATE, stream), f"sharded {op} accumulate")
         self._mark(f"{op}_done")
 
     def run_phases(self, op: str, phases) -> None:
         """Only the given phases of one execute (redset_hip_sharded_execute_phase),
         in order, with no marks: the bench times the decode on slices already in
-        place (PHASE_COMPUTE) and the exchange (PHASE_GATHER, PHASE_RETURN) apart,
-        as BASELINE.md's C4 asks."""
+        place (PHASE_COMPUTE + PHASE_ACCUMULATE) and the exchange (PHASE_GATHER,
+        PHASE_RETURN) apart, as BASELINE.md's C4 asks."""
         L = _lib.load()
         h = self._plans[op]
         stream = torch.cuda.current_stream().cuda_stream if self.device.type == "cuda" else None
@@ -412,9 +458,14 @@ class ShardedSetRunner:
 
     def report(self, step_seconds: float, op: str = "step") -> dict:
         tname = type(self._transport).__name__
-        coll = {"encode": f"{tname}: grouped P2P, data slices in, parity slices back (redset_hip_rs_sharded_plan)",
-                "rebuild": f"{tname}: grouped P2P, decode inputs' slices in, rebuilt slices back to their hosts "
-                           "(redset_hip_rs_sharded_plan)"}
+
+        def what(o, gather_text):
+            if o in self._plans and self.shape(o)["shape"] == "reduce":
+                return (f"{tname}: grouped P2P, partial sums of each GPU's own inputs to the outputs' hosts "
+                        "(redset_hip_rs_sharded_plan_ex, REDUCE shape)")
+            return f"{tname}: grouped P2P, {gather_text} (redset_hip_rs_sharded_plan_ex, GATHER shape)"
+        coll = {"encode": what("encode", "data slices in, parity slices back"),
+                "rebuild": what("rebuild", "decode inputs' slices in, rebuilt slices back to their hosts")}
         phases = self.phase_ms() if self.timing else None
         ops = ["encode", "rebuild"] if op == "step" else [op]
         msgs = {}
@@ -431,6 +482,9 @@ class ShardedSetRunner:
         out = {
             "exchange": {
                 "bytes_sent_per_gpu_per_step": self.exchanged_bytes(op),
+                # the shape each plan took and both shapes' counts (busiest
+                # GPU's max(sent, received) per execute, every GPU's view)
+                "shape": {o: self.shape(o) for o in ops if o in self._plans},
                 "messages_per_gpu": msgs,
                 "column_slice_bytes": self.W,
                 "collective": coll.get(op, coll["encode"] + "; " + coll["rebuild"]),
@@ -443,7 +497,7 @@ class ShardedSetRunner:
             # bounds the sharded rebuild; compare with xGMI, 7 links per GPU)
             i = self.info(op)
             g_ms = phases.get(f"{op}_start->gathered")
-            r_ms = phases.get(f"{op}_computed->done")
+            r_ms = phases.get(f"{op}_computed->returned")
             out["exchange"]["gather_send_GBps_rank0"] = (round(i["gather_bytes_sent"] / (g_ms * 1e-3) / 1e9, 1)
                                                          if g_ms else None)
             out["exchange"]["return_send_GBps_rank0"] = (round(i["return_bytes_sent"] / (r_ms * 1e-3) / 1e9, 1)

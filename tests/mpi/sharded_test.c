@@ -27,6 +27,14 @@
  * (redset_hip_*_sharded_plan_on with the complementary mask; the others take
  * slices 0 .. K - 1 of W = ceil(C / K)); they still host members, send their
  * cells and receive their outputs.
+ * SHARDED_TEST_SHAPE=gather|reduce|auto: plan through redset_hip_*_sharded_plan_ex
+ * with that exchange shape (REDSET_HIP_SHAPE_*; CPU mode: the partial sums'
+ * combines go to the oracle's multadd); every process prints the shape it
+ * planned and both shapes' byte counts.
+ * SHARDED_TEST_TRANSPORT=rccl: the RCCL transport (transport_rccl.c) instead
+ * of MPI's; the unique id goes out by MPI_Bcast. On the one-GPU test box and
+ * on the CPU this runs against tests/rcclstub (LD_LIBRARY_PATH), which
+ * accepts any number of ranks per GPU.
  * Placement: `world` sets of p members, member m on process (m * 7 + 3) %
  * world (SHARDED_TEST_SEED=<s>: on a pseudo-random process), hosted slots in
  * ascending member order. Exit 0 iff every process
@@ -101,6 +109,27 @@ static int oracle_run(void* ctx, int kind, int missing, const int* lost, unsigne
   free(lf);
   free(pr);
   return rc;
+}
+
+/* the partial-sum shape's combines on the CPU: the oracle's multadd
+ * (src/redset_reedsolomon_common.c:786-819) per output and input */
+static int oracle_combine(void* ctx, const redset_hip_combine_job* jobs, int njobs, size_t n, void* stream) {
+  (void) ctx;
+  (void) stream;
+  if (ME == FAIL_COMPUTE) return 1; /* SHARDED_TEST_FAIL_COMPUTE: the encode's first combine fails */
+  for (int k = 0; k < njobs; ++k) {
+    const redset_hip_combine_job* J = &jobs[k];
+    for (int j = 0; j < J->nout; ++j) {
+      if (!J->accumulate) memset(J->out[j], 0, n);
+      for (int i = 0; i < J->nin; ++i)
+        if (J->coef[j * J->nin + i]) ro_rs_multadd(ORACLE, n, J->out[j], J->coef[j * J->nin + i], J->in[i]);
+    }
+  }
+  return 0;
+}
+
+static const char* shape_name(int s) {
+  return s == REDSET_HIP_SHAPE_REDUCE ? "reduce" : s == REDSET_HIP_SHAPE_GATHER ? "gather" : "auto";
 }
 
 int main(int argc, char** argv) {
@@ -218,9 +247,39 @@ int main(int argc, char** argv) {
   }
   redset_hip_sharded *enc = NULL, *reb = NULL;
   const redset_hip_compute* cp = gpu ? NULL : &comp;
-  int ok = (XOR || redset_hip_rs_create(P, E, &rs) == 0) &&
-           redset_hip_mpi_transport_create(MPI_COMM_WORLD, host_slabs ? 2 : gpu ? 1 : 0, &tr, &th) == 0;
-  if (ok && XOR)
+  const char* tenv = getenv("SHARDED_TEST_TRANSPORT");
+  const int use_rccl = tenv && strcmp(tenv, "rccl") == 0;
+  redset_hip_rccl* rh = NULL;
+  int ok = XOR || redset_hip_rs_create(P, E, &rs) == 0;
+  if (ok && use_rccl) {
+    unsigned char uid[128];
+    memset(uid, 0, sizeof(uid));
+    int got = me != 0 || redset_hip_rccl_unique_id(uid) == 0, all_got = 0;
+    MPI_Allreduce(&got, &all_got, 1, MPI_INT, MPI_LAND, MPI_COMM_WORLD);
+    MPI_Bcast(uid, 128, MPI_BYTE, 0, MPI_COMM_WORLD);
+    ok = all_got && redset_hip_rccl_transport_create(uid, world, me, &tr, &rh) == 0;
+  } else if (ok) {
+    ok = redset_hip_mpi_transport_create(MPI_COMM_WORLD, host_slabs ? 2 : gpu ? 1 : 0, &tr, &th) == 0;
+  }
+  const char* shape_env = getenv("SHARDED_TEST_SHAPE");
+  redset_hip_sharded_opts opts;
+  memset(&opts, 0, sizeof(opts));
+  opts.struct_size = sizeof(opts);
+  opts.shape = !shape_env ? REDSET_HIP_SHAPE_AUTO
+               : strcmp(shape_env, "reduce") == 0 ? REDSET_HIP_SHAPE_REDUCE
+               : strcmp(shape_env, "gather") == 0 ? REDSET_HIP_SHAPE_GATHER
+                                                  : REDSET_HIP_SHAPE_AUTO;
+  opts.compute_on = getenv("SHARDED_TEST_IDLE") ? on : NULL;
+  opts.compute = cp;
+  opts.combine = gpu ? NULL : oracle_combine;
+  if (ok && shape_env && XOR)
+    ok = redset_hip_xor_sharded_plan_ex(P, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, &tr, &opts, &enc) == 0 &&
+         (missing == 0 ||
+          (missing == 1 && redset_hip_xor_sharded_plan_ex(P, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, &tr, &opts, &reb) == 0));
+  else if (ok && shape_env)
+    ok = redset_hip_rs_sharded_plan_ex(rs, REDSET_HIP_PLAN_RS_ENCODE, 0, NULL, &L, &tr, &opts, &enc) == 0 &&
+         (missing == 0 || redset_hip_rs_sharded_plan_ex(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, &tr, &opts, &reb) == 0);
+  else if (ok && XOR)
     ok = redset_hip_xor_sharded_plan_on(P, REDSET_HIP_PLAN_XOR_ENCODE, 0, &L, on, &tr, cp, &enc) == 0 &&
          (missing == 0 || (missing == 1 && redset_hip_xor_sharded_plan_on(P, REDSET_HIP_PLAN_XOR_REBUILD, lost[0], &L, on,
                                                                             &tr, cp, &reb) == 0));
@@ -229,6 +288,16 @@ int main(int argc, char** argv) {
          (missing == 0 ||
           redset_hip_rs_sharded_plan_on(rs, REDSET_HIP_PLAN_RS_REBUILD, missing, lost, &L, on, &tr, cp, &reb) == 0);
   if (!ok) fprintf(stderr, "rank %d: setup: %s\n", me, redset_hip_last_error());
+  for (int i = 0; ok && shape_env && i < 2; ++i) {
+    redset_hip_sharded* pl = i == 0 ? enc : reb;
+    redset_hip_sharded_shape_info si;
+    if (!pl || redset_hip_sharded_get_shape(pl, &si, sizeof(si)) != 0) continue;
+    printf("rank %d: %s shape %s (asked %s): gather busiest %llu B, reduce busiest %llu B (possible %d), "
+           "sent %llu / %llu B, scratch %llu of %llu B\n",
+           me, i == 0 ? "encode" : "rebuild", shape_name(si.shape), shape_name(opts.shape), si.gather_busiest_bytes,
+           si.reduce_busiest_bytes, si.reduce_possible, si.gather_bytes_sent, si.reduce_bytes_sent,
+           si.scratch_bytes_needed, si.scratch_bytes);
+  }
   int bad = 0;
   if (ok && redset_hip_sharded_execute(enc, stream) != 0) {
     fprintf(stderr, "rank %d: encode: %s\n", me, redset_hip_last_error());
@@ -290,7 +359,7 @@ int main(int argc, char** argv) {
       double t0 = MPI_Wtime();
       for (int i = 0; ok && i < reps; ++i) {
         if (mode == 0) ok = redset_hip_sharded_execute(reb, stream) == 0;
-        for (int ph = REDSET_HIP_PHASE_GATHER; ok && mode == 1 && ph <= REDSET_HIP_PHASE_RETURN; ++ph)
+        for (int ph = REDSET_HIP_PHASE_GATHER; ok && mode == 1 && ph <= REDSET_HIP_PHASE_ACCUMULATE; ++ph)
           ok = redset_hip_sharded_execute_phase(reb, ph, stream) == 0;
       }
       ok = ok && hipStreamSynchronize(stream) == hipSuccess;
@@ -310,6 +379,7 @@ int main(int argc, char** argv) {
   redset_hip_sharded_destroy(enc);
   redset_hip_sharded_destroy(reb);
   redset_hip_mpi_transport_destroy(th);
+  redset_hip_rccl_transport_destroy(rh);
   redset_hip_rs_destroy(rs);
   if (host_slabs) {
     (void) hipHostFree(dHD);

@@ -44,6 +44,20 @@ class OracleBackend:
         for v, a in zip(pv, pr):
             v[:, :n] = a.reshape(e, n)
 
+    def combine(self, jobs, n, bufs):
+        """The partial-sum shape's combines: out[j] = (out[j] ^) sum_i
+        coef[j][i] * in[i] by the oracle's multadd
+        (src/redset_reedsolomon_common.c:786-819)."""
+        for ins, outs, coef, acc in jobs:
+            iv = [bufs.view(a, n).numpy() for a in ins]
+            for j, a in enumerate(outs):
+                ov = bufs.view(a, n).numpy()
+                if not acc:
+                    ov[:] = 0
+                for i, x in enumerate(iv):
+                    if coef[j, i]:
+                        self.st.multadd(ov, int(coef[j, i]), x)
+
 
 def _free_port():
     with socket.socket() as s:
@@ -51,7 +65,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def _worker(rank, world, port, p, e, chunk, lost, outdir, sets=None):
+def _worker(rank, world, port, p, e, chunk, lost, outdir, sets=None, shape="gather"):
     import sys
 
     sys.path.insert(0, ROOT)
@@ -62,7 +76,7 @@ def _worker(rank, world, port, p, e, chunk, lost, outdir, sets=None):
     from redset_amd.dist import ShardedSetRunner
 
     runner = ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, device="cpu",
-                              backend=OracleBackend(p, e), seed=99, transport="torch", sets=sets)
+                              backend=OracleBackend(p, e), seed=99, transport="torch", sets=sets, shape=shape)
     if rank == 0:
         import json
 
@@ -82,7 +96,8 @@ def _worker(rank, world, port, p, e, chunk, lost, outdir, sets=None):
     with open(os.path.join(outdir, f"sent_{rank}.json"), "w") as f:
         import json
 
-        json.dump({"rebuild": runner.exchanged_bytes("rebuild"), "W": runner.W}, f)
+        json.dump({"rebuild": runner.exchanged_bytes("rebuild"), "W": runner.W,
+                   "shape": {o: runner.shape(o) for o in ("encode", "rebuild")}}, f)
     np.save(os.path.join(outdir, f"data2_{rank}.npy"), runner.D_host.numpy())
     np.save(os.path.join(outdir, f"par2_{rank}.npy"), runner.P_host.numpy())
     dist.barrier()
@@ -100,17 +115,44 @@ def _assemble(host_arrays, where, world, p, chunk, W, k, r):
     return np.concatenate(cells)
 
 
-@pytest.mark.parametrize("world,p,e,chunk,lost,sets", [
-    (2, 4, 2, 3000, [1], None), (2, 11, 3, 4096, [1, 2], None), (4, 11, 3, 2048, [1, 2], None),
-    (8, 11, 3, 4096, [1, 2], None),  # the driver's 8-GPU shape
-    (3, 5, 2, 1000, [0, 4], None),
+def _reduce_sent(p, e, lost, where, world, nsets, chunk, W):
+    """All GPUs' bytes of the partial-sum shape's rebuild, counted here from
+    the decode maps and the placement: one W-byte row per output cell,
+    remote contributor and slice with cell bytes (independent of sharded.c)."""
+    from redset_amd.codec import RSCodec
+
+    rs = RSCodec(p, e)
+    nslices = sum(1 for q in range(world) if q * W < chunk)
+    rows = 0
+    for k in range(nsets):
+        for c in range(p):
+            D = rs.decode_matrix(list(lost), c)
+            for i, l in enumerate(lost):
+                host = where[str(k * p + l)][0]
+                contrib = {where[str(k * p + s)][0] for s in range(p) if D[i, s]}
+                rows += len(contrib - {host}) * nslices
+    rs.close()
+    return rows * W
+
+
+@pytest.mark.parametrize("world,p,e,chunk,lost,sets,shape", [
+    (2, 4, 2, 3000, [1], None, "gather"), (2, 11, 3, 4096, [1, 2], None, "gather"),
+    (4, 11, 3, 2048, [1, 2], None, "gather"),
+    (8, 11, 3, 4096, [1, 2], None, "gather"),  # the driver's 8-GPU shape
+    (3, 5, 2, 1000, [0, 4], None, "gather"),
     # one set spread over every GPU (strong scaling, BASELINE.md's C4)
-    (2, 11, 3, 4096, [1, 2], 1), (3, 5, 2, 1000, [0, 4], 1), (8, 11, 3, 4096, [1, 2], 1)])
-def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost, sets):
+    (2, 11, 3, 4096, [1, 2], 1, "gather"), (3, 5, 2, 1000, [0, 4], 1, "gather"), (8, 11, 3, 4096, [1, 2], 1, "gather"),
+    # the partial-sum shape (each GPU sends partial sums of its own inputs to
+    # the outputs' hosts), forced, and AUTO's choice at the bench's shapes
+    (2, 11, 3, 4096, [1, 2], None, "reduce"), (4, 11, 3, 2048, [1, 2], None, ("auto", "reduce")),
+    (3, 5, 2, 1000, [0, 4], None, "reduce"), (2, 11, 3, 4096, [1, 2], 1, "reduce"),
+    (2, 11, 3, 4096, [1, 2], None, "auto"), (4, 11, 3, 2048, [1, 2], None, "auto"),
+    (8, 11, 3, 4096, [1, 2], None, "auto"), (8, 11, 3, 4096, [1, 2], 1, "auto")])
+def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost, sets, shape):
     port = _free_port()
     nsets = world if sets is None else sets
     with tempfile.TemporaryDirectory() as td:
-        mp.spawn(_worker, args=(world, port, p, e, chunk, lost, td, sets), nprocs=world, join=True)
+        mp.spawn(_worker, args=(world, port, p, e, chunk, lost, td, sets, shape), nprocs=world, join=True)
         load = lambda name: [np.load(os.path.join(td, f"{name}_{g}.npy")) for g in range(world)]
         data, par, data2, par2 = load("data"), load("par"), load("data2"), load("par2")
         W = data[0].shape[-1]
@@ -124,12 +166,26 @@ def test_sharded_encode_rebuild_gloo(oracle, world, p, e, chunk, lost, sets):
 
         need_d, need_p = rebuild_inputs(p, e, lost)
         cells_in = sum(int(need_d[r].sum() + need_p[r].sum()) for r in range(p))
-        want_sent = nsets * (world - 1) * W * (cells_in + len(lost) * p)
-        sent = 0
+        gather_sent = nsets * (world - 1) * W * (cells_in + len(lost) * p)
+        reduce_sent = _reduce_sent(p, e, lost, where, world, nsets, chunk, W)
+        sent, shapes = 0, []
         for g in range(world):
             with open(os.path.join(td, f"sent_{g}.json")) as f:
-                sent += json.load(f)["rebuild"]
-        assert sent == want_sent
+                rec = json.load(f)
+            sent += rec["rebuild"]
+            shapes.append(rec["shape"])
+        got = {sh["rebuild"]["shape"] for sh in shapes}
+        assert len(got) == 1, shapes  # every GPU planned the same shape
+        got = got.pop()
+        want_shape = shape if isinstance(shape, str) else shape[1]
+        if want_shape != "auto":
+            assert got == want_shape
+        else:
+            # AUTO: the shape whose busiest GPU moves fewer bytes (ties: gather)
+            sh = shapes[0]["rebuild"]
+            better = sh["reduce_possible"] and sh["reduce_busiest_bytes"] < sh["gather_busiest_bytes"]
+            assert got == ("reduce" if better else "gather"), sh
+        assert sent == (reduce_sent if got == "reduce" else gather_sent), (got, sent, gather_sent, reduce_sent)
         assert cells_in == p * (p - e)
         st = oracle.OracleRS(p, e)
         for k in range(nsets):

@@ -205,3 +205,144 @@ def test_sharded_compute_failure_keeps_the_exchange_going(scheme, np_, p, e, fai
     assert res.returncode != 0, res.stdout + res.stderr
     assert f"rank {fail}: encode:" in res.stderr, res.stderr
     assert "compute callback failed" in res.stderr, res.stderr
+
+
+# ---- the partial-sum shape (REDSET_HIP_SHAPE_REDUCE) ----------------------
+
+
+def _shapes(stdout):
+    """(op, planned shape, gather busiest, reduce busiest) per printed line"""
+    import re
+
+    return [(m.group(1), m.group(2), int(m.group(3)), int(m.group(4)))
+            for m in re.finditer(r"rank \d+: (encode|rebuild) shape (\w+) \(asked \w+\): gather busiest (\d+) B, "
+                                 r"reduce busiest (\d+) B", stdout)]
+
+
+@pytest.mark.parametrize("shape", ["reduce", "auto"])
+@pytest.mark.parametrize("scheme,np_,p,e,chunk,lost", [
+    ("rs", 2, 11, 3, 3001, [1, 2]),     # configs[3]'s shape
+    ("rs", 3, 11, 3, 4096, [1, 2]),
+    ("rs", 2, 20, 4, 777, [0, 5, 19]),  # configs[4]'s shape
+    ("rs", 3, 5, 2, 1000, [0, 4]),
+    ("rs", 2, 6, 3, 1, [2]),            # one-byte chunk: one slice with bytes
+    ("rs", 6, 7, 2, 1, [4, 6]),
+    ("xor", 3, 8, 1, 3001, [3]),        # configs[1]'s shape
+    ("xor", 4, 12, 1, 1, [5]),
+])
+def test_reduce_shape_matches_oracle(oracle, shape, scheme, np_, p, e, chunk, lost):
+    """The sharded plan's partial-sum shape (sharded.c plan_reduce): every
+    process combines ITS members' cells into partial outputs with the stripe's
+    own coefficients (the oracle's multadd does the combines here), sends one
+    partial per output it feeds to the output's host, which XORs them in.
+    Parity after the encode and the lost members after the rebuild against the
+    oracle's whole-set answer; every process plans the same shape from the
+    same byte counts, and AUTO takes the one whose busiest process moves
+    fewer bytes."""
+    if not _have():
+        pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", DRIVER, str(p), str(e), str(chunk)] + [str(x) for x in lost]
+    env = {**os.environ, "SHARDED_TEST_SHAPE": shape}
+    if scheme == "xor":
+        env["SHARDED_TEST_SCHEME"] = "xor"
+    res = run_group(cmd, 120, env=env, cwd="/tmp")
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert res.stdout.count("rebuild gather") == np_
+    lines = _shapes(res.stdout)
+    assert len(lines) == 2 * np_, res.stdout
+    for op in ("encode", "rebuild"):
+        mine = {x[1:] for x in lines if x[0] == op}
+        assert len(mine) == 1, mine  # the same plan everywhere
+        planned, gb, rb = mine.pop()
+        if shape == "reduce":
+            assert planned == "reduce"
+        else:
+            assert planned == ("reduce" if rb < gb else "gather"), (op, planned, gb, rb)
+
+
+def test_reduce_shape_moves_fewer_bytes_at_the_bench_shape(oracle):
+    """configs[3] at N = 2, two sets of RS(8+3) with members 1, 2 lost: the
+    rebuild's busiest process sends 2.5x fewer bytes as partial sums than as
+    gathered input slices."""
+    if not _have():
+        pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
+    cmd = [MPIRUN, "-np", "2", "-host", "localhost", DRIVER, "11", "3", "4096", "1", "2"]
+    res = run_group(cmd, 120, env={**os.environ, "SHARDED_TEST_SHAPE": "auto"}, cwd="/tmp")
+    assert res.returncode == 0, res.stdout + res.stderr
+    reb = [x for x in _shapes(res.stdout) if x[0] == "rebuild"]
+    assert reb and all(x[1] == "reduce" for x in reb), reb
+    _, _, gb, rb = reb[0]
+    assert gb == 2.5 * rb, (gb, rb)
+
+
+@pytest.mark.parametrize("seed", range(16))
+def test_reduce_shape_random(oracle, seed):
+    """Seeded random shapes, erasures, chunks, worlds 2..8 and placements
+    through the partial-sum shape (odd seeds forced, even seeds AUTO) against
+    the oracle. A forced plan whose partial sums do not fit the gathered
+    slabs must fail on every process with that reason, not hang."""
+    if not _have():
+        pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
+    import numpy as np
+
+    rng = np.random.default_rng(9100 + seed)
+    np_ = int(rng.integers(2, 9))
+    p = int(rng.integers(2, 24))
+    e = int(rng.integers(1, min(p - 1, 6) + 1))
+    chunk = int(rng.choice([1, 255, 256, 257, int(rng.integers(2, 5000))]))
+    m = int(rng.integers(1, e + 1))
+    lost = sorted(rng.choice(p, size=m, replace=False).tolist())
+    shape = "reduce" if seed % 2 else "auto"
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", DRIVER, str(p), str(e), str(chunk)] + [str(x) for x in lost]
+    env = {**os.environ, "SHARDED_TEST_SEED": str(seed), "SHARDED_TEST_SHAPE": shape}
+    res = run_group(cmd, 120, env=env, cwd="/tmp")
+    if res.returncode != 0 and shape == "reduce" and res.stderr.count("do not fit the gathered slabs") == np_:
+        return
+    assert res.returncode == 0, (np_, p, e, chunk, lost, res.stdout + res.stderr)
+    assert res.stdout.count("rebuild gather") == np_
+
+
+def test_reduce_shape_compute_failure_keeps_the_exchange_going():
+    """A process whose combines fail still runs the partial-sum exchange its
+    peers wait in; every process returns and the AND fails."""
+    if not _have():
+        pytest.skip("needs MPICH (mpirun) and libredset_hip_mpi.so")
+    cmd = [MPIRUN, "-np", "3", "-host", "localhost", DRIVER, "11", "3", "5000"]
+    env = {**os.environ, "SHARDED_TEST_FAIL_COMPUTE": "1", "SHARDED_TEST_SHAPE": "reduce"}
+    res = run_group(cmd, 60, env=env, cwd="/tmp")
+    assert res.returncode != 0, res.stdout + res.stderr
+    assert "rank 1: encode:" in res.stderr and "combine callback failed" in res.stderr, res.stderr
+
+
+# ---- the RCCL transport at world > 1, over the test stand-in -------------
+
+HIPSTUB = os.path.join(ROOT, "tests", "mpi", "build", "libhipstub.so")
+RCCLSTUB_DIR = os.path.join(ROOT, "tests", "rcclstub", "lib")
+
+
+@pytest.mark.parametrize("shape", ["gather", "reduce"])
+@pytest.mark.parametrize("scheme,np_,p,e,chunk,lost", [
+    ("rs", 2, 11, 3, 30001, [1, 2]), ("rs", 3, 11, 3, 4096, [1, 2]), ("rs", 4, 6, 2, 999, [0, 5]),
+    ("xor", 3, 8, 1, 3001, [3])])
+def test_rccl_transport_at_world_above_one_on_cpu(oracle, shape, scheme, np_, p, e, chunk, lost):
+    """transport_rccl.c (grouped ncclSend / ncclRecv, local copies) at world
+    2-4, on the CPU: tests/rcclstub's librccl.so.1 moves the messages through
+    shared memory and tests/mpi/hipstub.c stands in for the HIP runtime, so
+    the transport's grouping, peer matching and message lengths are checked
+    against the oracle here; tests/test_gpu_rccl_stub.py runs the same on
+    the GPU."""
+    if not _have() or not os.path.exists(os.path.join(RCCLSTUB_DIR, "librccl.so.1")) or not os.path.exists(HIPSTUB):
+        pytest.skip("needs MPICH, tests/rcclstub and tests/mpi/build/libhipstub.so")
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", "-genv", "LD_PRELOAD", HIPSTUB, DRIVER, str(p), str(e),
+           str(chunk)] + [str(x) for x in lost]
+    ld = os.environ.get("LD_LIBRARY_PATH")
+    env = {**os.environ, "SHARDED_TEST_TRANSPORT": "rccl", "SHARDED_TEST_SHAPE": shape,
+           "LD_LIBRARY_PATH": RCCLSTUB_DIR + (":" + ld if ld else "")}
+    if scheme == "xor":
+        env["SHARDED_TEST_SCHEME"] = "xor"
+    res = run_group(cmd, 120, env=env, cwd="/tmp")
+    if res.returncode != 0 and shape == "reduce" and "do not fit" in res.stderr:
+        pytest.skip("the partial sums do not fit this placement's scratch")
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert res.stdout.count("rebuild gather") == np_
+    assert not [f for f in os.listdir("/dev/shm") if f.startswith("rcclstub_")], "stand-in left shared memory"

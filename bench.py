@@ -62,7 +62,7 @@ def parse():
                     help="MiB of padding after every cell in HBM; -1 (default) = the library's recommended "
                          "stride (redset_hip_cell_stride: 16 MiB after 64 MiB cells, breaking their 2^26-byte "
                          "aliasing, +2.0%% with stripes in sequence, profiles/r02_ab_cell_pad.txt)")
-    ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port beside (rank 0, N=1)")
+    ap.add_argument("--cpu-baseline", type=int, default=1, help="1: time the CPU port beside (rank 0, every N)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU sample duration (RS; XOR gets half)")
     ap.add_argument("--cpu-chunk-mib", type=float, default=0.0,
                     help="chunk of the CPU baseline's set (0: the GPU workload's own chunk)")
@@ -73,6 +73,13 @@ def parse():
     ap.add_argument("--sharded-timeout", type=float, default=150.0,
                     help="seconds the sharded leg may take before the main line is printed without it")
     ap.add_argument("--xor", type=int, default=1, help="also time the XOR set of configs[1] (rank 0)")
+    ap.add_argument("--sharded-shape", default="auto", choices=["auto", "gather", "reduce"],
+                    help="the sharded leg's exchange shape (include/redset_hip.h REDSET_HIP_SHAPE_*): auto lets "
+                         "the planner take the one whose busiest GPU moves fewer bytes")
+    ap.add_argument("--sharded-transport", default="", choices=["", "rccl", "torch"],
+                    help="the sharded leg's transport (default: RCCL under an nccl process group or at N = 1, "
+                         "else the torch.distributed callback); tests force rccl under gloo with the test twin "
+                         "and tests/rcclstub")
     ap.add_argument("--pairs", type=int, default=1,
                     help="also time the rebuild of every pair of erased members (rank 0; SURVEY.md §8d worst case)")
     ap.add_argument("--dist-backend", default="nccl",
@@ -419,8 +426,8 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
 
     import redset_amd
     from redset_amd import dist as rdist
-    from redset_amd._lib import PHASE_COMPUTE as L_PHASE_COMPUTE, PHASE_GATHER as L_PHASE_GATHER
-    from redset_amd._lib import PHASE_RETURN as L_PHASE_RETURN
+    from redset_amd._lib import PHASE_ACCUMULATE as L_PHASE_ACCUMULATE, PHASE_COMPUTE as L_PHASE_COMPUTE
+    from redset_amd._lib import PHASE_GATHER as L_PHASE_GATHER, PHASE_RETURN as L_PHASE_RETURN
 
     dist_on = world > 1
     dev = "cuda" if (not dist_on or dist.get_backend() == "nccl") else "cpu"
@@ -431,7 +438,9 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
             dist.all_reduce(t, op=op)
         return t.item()
 
-    runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank)
+    runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, shape=args.sharded_shape,
+                                    transport=args.sharded_transport or None)
+    shape = runner.shape("rebuild")
     runner.encode()
     snap = runner.lost_snapshot()
     runner.erase()
@@ -456,18 +465,20 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     sent_max = reduce(sent_mine, dist.ReduceOp.MAX, torch.float64)
     info = runner.info("rebuild")
     recv_max = reduce(float(info["gather_bytes_recv"] + info["return_bytes_recv"]), dist.ReduceOp.MAX, torch.float64)
-    # untimed diagnostic: the same rebuild with its three phases one after
+    # untimed diagnostic: the same rebuild with its four phases one after
     # another (no overlap across sets), timed apart by events on rank 0
     pipelined_event_ms = runner.phase_ms().get("rebuild_start->done")
     runner.phased = True
     timed(lambda i: runner.rebuild(), 3, 1, dist_on, before=runner.reset_timing)
     phases = runner.phase_ms()
     compute_ms = phases.get("rebuild_gathered->computed")
+    if compute_ms is not None and phases.get("rebuild_returned->done") is not None:
+        compute_ms = round(compute_ms + phases["rebuild_returned->done"], 4)  # + the accumulate
     # BASELINE.md's C4 as it states it: the column-sharded decode on N GPUs
     # with every GPU's slices already in place, and the RCCL exchange (gather
     # + return) timed separately -- each K steps bracketed like the step,
-    # max over ranks
-    d_step = timed(lambda i: runner.run_phases("rebuild", [L_PHASE_COMPUTE]), args.steps, warm,
+    # max over ranks (partial-sum shape: the combines, and its one exchange)
+    d_step = timed(lambda i: runner.run_phases("rebuild", [L_PHASE_COMPUTE, L_PHASE_ACCUMULATE]), args.steps, warm,
                    dist_on) / args.steps
     x_step = timed(lambda i: runner.run_phases("rebuild", [L_PHASE_GATHER, L_PHASE_RETURN]), args.steps,
                    min(warm, args.warmup), dist_on) / args.steps
@@ -489,7 +500,14 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
         "ms_per_step": round(s_step * 1e3, 4),
         "bit_exact": bool(ok),
         "transport": type(runner._transport).__name__ + ("" if dist_on else " (world 1: no messages)"),
-        "schedule": "sets pipelined: set k+1's gather overlaps set k's gf_mac (redset_hip_sharded_execute)",
+        # the exchange's shape, chosen by the planner from its byte counts
+        # (include/redset_hip.h REDSET_HIP_SHAPE_*): gather the inputs' column
+        # slices, or send each GPU's partial sums of its own inputs
+        "shape": shape["shape"],
+        "schedule": ("sets pipelined: set k+1's gather overlaps set k's gf_mac (redset_hip_sharded_execute)"
+                     if shape["shape"] == "gather" else
+                     "sets pipelined: set k's partial-sum exchange overlaps set k+1's combines "
+                     "(redset_hip_sharded_execute)"),
         "pipelined_event_ms_rank0": pipelined_event_ms,
         "roofline": {
             "bound": "xgmi",
@@ -521,6 +539,13 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
                 max(sent_max, recv_max) / (link_peak * 1e9) if dist_on else 0.0,
                 info["compute_bytes"] / (MODEL_GF_MAC_GBPS * 1e9)) / 1e9, 1),
             "note": f"{XGMI_LINK_GBPS:g} GB/s per xGMI link (platform figure), gf_mac {MODEL_GF_MAC_GBPS:g} GB/s",
+            # both shapes' busiest GPU (max over GPUs of max(sent, received))
+            # at the same link rate: what each would cost on the fabric
+            "xgmi_ms_by_shape": {
+                "gather": round(shape["gather_busiest_bytes"] / (link_peak * 1e9) * 1e3, 4) if dist_on else 0.0,
+                "reduce": (round(shape["reduce_busiest_bytes"] / (link_peak * 1e9) * 1e3, 4)
+                           if dist_on and shape["reduce_possible"] else None),
+            },
         },
         # C4's decode alone, slices in place (all GPUs, max over ranks)
         "decode": {
@@ -569,9 +594,11 @@ def one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak):
 
     import redset_amd
     from redset_amd import dist as rdist
-    from redset_amd._lib import PHASE_COMPUTE, PHASE_GATHER, PHASE_RETURN
+    from redset_amd._lib import PHASE_ACCUMULATE, PHASE_COMPUTE, PHASE_GATHER, PHASE_RETURN
 
-    runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, sets=1)
+    runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, sets=1, shape=args.sharded_shape,
+                                    transport=args.sharded_transport or None)
+    shape = runner.shape("rebuild")
     runner.timing = False
     runner.encode()
     snap = runner.lost_snapshot()
@@ -580,7 +607,8 @@ def one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak):
     step = timed(lambda i: runner.rebuild(), args.steps, warm, dist_on) / args.steps
     torch.cuda.synchronize()
     ok = reduce(1 if runner.matches(snap) and redset_amd.hang_faults() == 0 else 0, dist.ReduceOp.MIN, torch.int32)
-    d_step = timed(lambda i: runner.run_phases("rebuild", [PHASE_COMPUTE]), args.steps, warm, dist_on) / args.steps
+    d_step = timed(lambda i: runner.run_phases("rebuild", [PHASE_COMPUTE, PHASE_ACCUMULATE]), args.steps, warm,
+                   dist_on) / args.steps
     x_step = timed(lambda i: runner.run_phases("rebuild", [PHASE_GATHER, PHASE_RETURN]), args.steps,
                    min(warm, args.warmup), dist_on) / args.steps
     total = runner.total_algorithmic_bytes("rebuild")
@@ -595,6 +623,9 @@ def one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak):
         "frac_of_hbm": round(total / step / 1e9 / peak, 6),
         "ms_per_step": round(step * 1e3, 4),
         "bit_exact": bool(ok),
+        "shape": shape["shape"],
+        "busiest_gpu_bytes_by_shape": {"gather": shape["gather_busiest_bytes"],
+                                       "reduce": shape["reduce_busiest_bytes"] if shape["reduce_possible"] else None},
         "decode": {"value": round(total / d_step / 1e9, 2), "frac_of_hbm": round(total / d_step / 1e9 / peak, 6),
                    "ms_per_step": round(d_step * 1e3, 4)},
         "exchange_only": {"ms_per_step": round(x_step * 1e3, 4),
@@ -875,7 +906,8 @@ def main():
         # A hung exchange or final barrier cannot raise: a watchdog then
         # prints the main line (with the sharded leg marked timed out) and
         # ends every rank with a non-zero status.
-        watchdog = threading.Timer(args.sharded_timeout, sharded_expired, (result, rank, args.sharded_timeout))
+        limit = args.sharded_timeout + (3 * args.cpu_seconds + 60 if args.cpu_baseline else 0)
+        watchdog = threading.Timer(limit, sharded_expired, (result, rank, limit))
         watchdog.daemon = True
         watchdog.start()
     if args.sharded:
@@ -887,8 +919,18 @@ def main():
             result["sharded"] = sharded_leg(args, p, e, chunk, lost, world, rank)
         except Exception as exc:  # noqa: BLE001 -- reported, not swallowed
             result["sharded"] = {"error": f"{type(exc).__name__}: {exc}"}
-    if args.cpu_baseline and rank == 0 and not dist_on:
+        # configs[3]'s scaling number next to `value`: the
+        # exchange-bearing step, where SCALE's reader looks first
+        sv = result["sharded"].get("value")
+        result["config"]["scaling_value_GBps"] = sv
+        result["scaling_value_GBps"] = sv
+    if args.cpu_baseline and rank == 0:
+        # at N > 1 too, after every collective of the legs and under the
+        # watchdog (its limit has the CPU leg's seconds added): the other
+        # ranks wait in the final barrier meanwhile
         result["cpu_baseline"] = cpu_baseline(p, e, lost, args.cpu_seconds, cpu_chunk)
+        if dist_on and args.xor and "xor" in result:
+            result["xor"]["cpu_baseline"] = cpu_baseline_xor(8, 3, args.cpu_seconds / 2, cpu_chunk)
     emit(result, rank)
     if dist_on:
         dist.barrier()

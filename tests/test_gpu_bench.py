@@ -48,8 +48,16 @@ def _check_sharded(sh, world):
     assert sh["exchange_only"]["ms_per_step"] >= 0
     msgs = sh["exchange"]["messages_per_gpu"]["rebuild"]
     if world > 1:
-        # every GPU gathers slices from its peer and returns rebuilt slices
-        assert msgs["gather_messages"] > 0 and msgs["return_messages"] > 0, msgs
+        if sh["shape"] == "gather":
+            # every GPU gathers slices from its peer and returns rebuilt slices
+            assert msgs["gather_messages"] > 0 and msgs["return_messages"] > 0, msgs
+        else:
+            # partial sums of each GPU's own inputs to the outputs' hosts: one exchange
+            assert sh["shape"] == "reduce" and msgs["gather_messages"] == 0 and msgs["return_messages"] > 0, msgs
+        # the planner's choice: the shape whose busiest GPU moves fewer bytes
+        by = sh["model"]["xgmi_ms_by_shape"]
+        if by["reduce"] is not None:
+            assert sh["shape"] == ("reduce" if by["reduce"] < by["gather"] else "gather"), by
         assert sh["exchange"]["bytes_sent_per_gpu_per_step"] > 0
         assert sh["exchange_only"]["send_GBps_per_gpu"] > 0, sh["exchange_only"]
         # BASELINE.md C4 word for word: one set over every GPU (strong scaling)
@@ -64,11 +72,47 @@ def _check_sharded(sh, world):
 
 @pytest.mark.timeout(420)
 def test_bench_two_ranks_self_launched_over_gloo():
-    line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--sharded-timeout", "300"] + SMALL, 400)
+    """...and, at N > 1 too, the CPU baseline on rank 0 and configs[3]'s
+    scaling number (sharded.value) next to `value`."""
+    i = SMALL.index("--cpu-baseline")
+    args = SMALL[:i] + ["--cpu-baseline", "1", "--cpu-seconds", "1"] + SMALL[i + 2:]
+    line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--sharded-timeout", "300"] + args, 400)
     assert line["n_gpus"] == 2 and line["round_trip_bit_exact"] is True
     assert line["config"]["sets"] == 2
     assert line["config"]["scaling_value"].startswith("sharded.value")
     _check_sharded(line["sharded"], 2)
+    assert line["config"]["scaling_value_GBps"] == line["sharded"]["value"] == line["scaling_value_GBps"]
+    cb = line["cpu_baseline"]
+    assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1, cb
+
+
+@pytest.mark.timeout(420)
+@pytest.mark.parametrize("shape", ["gather", "reduce"])
+def test_bench_two_ranks_over_the_rccl_transport(shape):
+    """The bench's N = 2 sharded leg as the 8-GPU node runs it -- RcclTransport,
+    grouped ncclSend / ncclRecv -- on this box's one GPU: the test twin loads
+    tests/rcclstub by path (REDSET_HIP_TEST_RCCL_LIBRARY; the real RCCL
+    refuses two ranks on one device), the process group is gloo. Each shape
+    once, bit-exact."""
+    twin = os.path.join(ROOT, "redset_amd", "lib_test", "libredset_hip.so")
+    stub = os.path.join(ROOT, "tests", "rcclstub", "lib", "librccl.so.1")
+    if not os.path.exists(twin) or not os.path.exists(stub):
+        pytest.skip("needs the test twin and tests/rcclstub")
+    old = {k: os.environ.get(k) for k in ("REDSET_HIP_LIBRARY", "REDSET_HIP_TEST_RCCL_LIBRARY")}
+    os.environ["REDSET_HIP_LIBRARY"] = twin
+    os.environ["REDSET_HIP_TEST_RCCL_LIBRARY"] = stub
+    try:
+        line = _bench(["--gpus", "2", "--dist-backend", "gloo", "--sharded-timeout", "300", "--sharded-transport",
+                       "rccl", "--sharded-shape", shape] + SMALL, 400)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+    _check_sharded(line["sharded"], 2)
+    assert line["sharded"]["transport"].startswith("RcclTransport"), line["sharded"]["transport"]
+    assert line["sharded"]["shape"] == shape
 
 
 @pytest.mark.timeout(300)

@@ -38,7 +38,7 @@ def _bench(args, timeout):
     return json.loads(lines[0])
 
 
-def _check_sharded(sh, world):
+def _check_sharded(sh, world, auto=True):
     assert "error" not in sh, sh
     assert sh["bit_exact"] is True
     assert sh["value"] > 0 and 0 < sh["frac_of_hbm"] < 1  # gloo moves tens of MB/s: a tiny fraction
@@ -56,7 +56,7 @@ def _check_sharded(sh, world):
             assert sh["shape"] == "reduce" and msgs["gather_messages"] == 0 and msgs["return_messages"] > 0, msgs
         # the planner's choice: the shape whose busiest GPU moves fewer bytes
         by = sh["model"]["xgmi_ms_by_shape"]
-        if by["reduce"] is not None:
+        if auto and by["reduce"] is not None:
             assert sh["shape"] == ("reduce" if by["reduce"] < by["gather"] else "gather"), by
         assert sh["exchange"]["bytes_sent_per_gpu_per_step"] > 0
         assert sh["exchange_only"]["send_GBps_per_gpu"] > 0, sh["exchange_only"]
@@ -110,7 +110,7 @@ def test_bench_two_ranks_over_the_rccl_transport(shape):
                 os.environ.pop(k, None)
             else:
                 os.environ[k] = v
-    _check_sharded(line["sharded"], 2)
+    _check_sharded(line["sharded"], 2, auto=False)
     assert line["sharded"]["transport"].startswith("RcclTransport"), line["sharded"]["transport"]
     assert line["sharded"]["shape"] == shape
 

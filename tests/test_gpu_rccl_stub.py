@@ -75,7 +75,7 @@ def test_sharded_rccl_transport_with_hip_kernels(shape, np_, p, e, chunk, lost):
 
 
 @pytest.mark.parametrize("mode", ["--gpu", "--gpu-host"])
-@pytest.mark.parametrize("np_,p,e,chunk,lost,scheme", [(2, 11, 3, 300_001, [1, 2], "rs"), (3, 5, 2, 40_000, [0, 4], "rs"),
+@pytest.mark.parametrize("np_,p,e,chunk,lost,scheme", [(2, 11, 3, 300_001, [1, 2], "rs"), (3, 6, 2, 40_000, [0, 4], "rs"),
                                                         (3, 8, 1, 65536, [3], "xor")])
 def test_sharded_reduce_shape_over_mpi(mode, np_, p, e, chunk, lost, scheme):
     """The partial-sum shape with the HIP combine plans (redset_hip_plan_combine)

@@ -19,6 +19,12 @@ algorithmic rebuild bytes over that. SCALE_rNN's sharded.value at each N is
 to be read against it. --one-set: one set spread over the N GPUs instead
 (the leg's `one_set`, BASELINE.md's C4 word for word).
 
+Both exchange shapes are planned (include/redset_hip.h REDSET_HIP_SHAPE_*):
+"gather" (every GPU gathers its column slice of each decode input and
+returns its slice of each output) and "reduce" (every GPU sends partial sums
+of its own inputs to the outputs' hosts); `auto` names the one the planner
+takes (the busiest GPU's max(sent, received) is smaller; ties: gather).
+
 usage: python tools/sharded_model.py [--chunk-mib 64] [--ranks 11] [--encoding 3] [--lost 1,2] [--one-set]
 """
 import argparse
@@ -47,7 +53,7 @@ def placement(p, lost, world, nsets):
     return where
 
 
-def plan_gpu(L, lib, rs, p, lost, chunk, world, rank, nsets):
+def plan_gpu(L, lib, rs, p, lost, chunk, world, rank, nsets, shape):
     where = placement(p, lost, world, nsets)
     nm = nsets * p
     host = (c_int * nm)(*[where[m][0] for m in range(nm)])
@@ -58,16 +64,42 @@ def plan_gpu(L, lib, rs, p, lost, chunk, world, rank, nsets):
                         base + (2 << 38), base + (3 << 38))
     tr = L.Transport(world, rank, ctypes.cast(L.EXCHANGE_FN(lambda *a: 0), c_void_p), None)
     cfn = L.COMPUTE_FN(lambda *a: 0)
+    kfn = L.COMBINE_FN(lambda *a: 0)
     comp = L.Compute(ctypes.cast(cfn, c_void_p), None)
+    opts = L.ShardedOpts()
+    opts.struct_size = ctypes.sizeof(L.ShardedOpts)
+    opts.shape = shape
+    opts.compute = ctypes.pointer(comp)
+    opts.combine = ctypes.cast(kfn, c_void_p)
     out = c_void_p()
     arr = (c_int * len(lost))(*lost)
-    if lib.redset_hip_rs_sharded_plan(rs, L.PLAN_RS_REBUILD, len(lost), arr, ctypes.byref(lay), ctypes.byref(tr),
-                                      ctypes.byref(comp), ctypes.byref(out)) != 0:
+    if lib.redset_hip_rs_sharded_plan_ex(rs, L.PLAN_RS_REBUILD, len(lost), arr, ctypes.byref(lay), ctypes.byref(tr),
+                                         ctypes.byref(opts), ctypes.byref(out)) != 0:
         raise RuntimeError(lib.redset_hip_last_error().decode())
     info = L.ShardedInfo()
     lib.redset_hip_sharded_get_info(out, ctypes.byref(info))
+    si = L.ShapeInfo()
+    lib.redset_hip_sharded_get_shape(out, ctypes.byref(si), ctypes.sizeof(si))
     lib.redset_hip_sharded_destroy(out)
-    return info.as_dict()
+    return info.as_dict(), si.as_dict()
+
+
+def price(rows, world, alg):
+    sent = max(r["gather_bytes_sent"] + r["return_bytes_sent"] for r in rows)
+    recv = max(r["gather_bytes_recv"] + r["return_bytes_recv"] for r in rows)
+    comp = max(r["compute_bytes"] for r in rows)
+    t_hbm = comp / (GF_MAC_REBUILD_GBPS * 1e9)
+    t_xgmi = max(sent, recv) / ((world - 1) * XGMI_LINK_GBPS * 1e9) if world > 1 else 0.0
+    step = max(t_hbm, t_xgmi)
+    return {
+        "per_gpu_max": {"bytes_sent": sent, "bytes_recv": recv, "compute_bytes": comp,
+                        "messages_sent": max(r["gather_messages"] + r["return_messages"] for r in rows)},
+        "seconds": {"hbm": round(t_hbm, 6), "xgmi": round(t_xgmi, 6)},
+        "bound": "xgmi" if t_xgmi > t_hbm else "hbm",
+        "model_ms_per_step": round(step * 1e3, 4),
+        "model_value_GBps": round(alg / step / 1e9, 1),
+        "model_frac_of_hbm": round(alg / step / 1e9 / (world * 8000.0), 4),
+    }
 
 
 def model(p, e, lost, chunk, world, one_set=False):
@@ -77,28 +109,24 @@ def model(p, e, lost, chunk, world, one_set=False):
     rs = c_void_p()
     lib.redset_hip_rs_create(p, e, ctypes.byref(rs))
     nsets = 1 if one_set else world
-    rows = [plan_gpu(L, lib, rs, p, lost, chunk, world, g, nsets) for g in range(world)]
-    lib.redset_hip_rs_destroy(rs)
-    sent = max(r["gather_bytes_sent"] + r["return_bytes_sent"] for r in rows)
-    recv = max(r["gather_bytes_recv"] + r["return_bytes_recv"] for r in rows)
-    comp = max(r["compute_bytes"] for r in rows)
-    t_hbm = comp / (GF_MAC_REBUILD_GBPS * 1e9)
-    t_xgmi = max(sent, recv) / ((world - 1) * XGMI_LINK_GBPS * 1e9) if world > 1 else 0.0
-    step = max(t_hbm, t_xgmi)
     alg = nsets * p * (p - e + len(lost)) * chunk
-    return {
+    out = {
         "n_gpus": world,
         "workload": (f"{nsets} set(s) of RS({p - e}+{e}) over {world} GPUs, chunk {chunk >> 20} MiB, rebuild {lost}, "
                      "members round-robin"),
-        "per_gpu_max": {"bytes_sent": sent, "bytes_recv": recv, "compute_bytes": comp,
-                        "messages_sent": max(r["gather_messages"] + r["return_messages"] for r in rows)},
-        "seconds": {"hbm": round(t_hbm, 6), "xgmi": round(t_xgmi, 6)},
-        "bound": "xgmi" if t_xgmi > t_hbm else "hbm",
-        "model_ms_per_step": round(step * 1e3, 4),
-        "model_value_GBps": round(alg / step / 1e9, 1),
-        "model_frac_of_hbm": round(alg / step / 1e9 / (world * 8000.0), 4),
         "ceilings": {"xgmi_GBps_per_link": XGMI_LINK_GBPS, "gf_mac_rebuild_GBps": GF_MAC_REBUILD_GBPS},
     }
+    plans = [plan_gpu(L, lib, rs, p, lost, chunk, world, g, nsets, L.SHAPE_AUTO) for g in range(world)]
+    out["auto"] = plans[0][1]["shape"]
+    out["reduce_possible"] = bool(plans[0][1]["reduce_possible"])
+    for name, sh in (("gather", L.SHAPE_GATHER), ("reduce", L.SHAPE_REDUCE)):
+        if name == "reduce" and not out["reduce_possible"]:
+            out[name] = None
+            continue
+        out[name] = price([plan_gpu(L, lib, rs, p, lost, chunk, world, g, nsets, sh)[0] for g in range(world)],
+                          world, alg)
+    lib.redset_hip_rs_destroy(rs)
+    return out
 
 
 def main():

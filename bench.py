@@ -578,27 +578,26 @@ def sharded_leg(args, p, e, chunk, lost, world, rank):
     runner.close()
     if dist_on:
         out["one_set"] = one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak)
+        # the shape not taken, measured (when the partial sums fit at all)
+        if args.sharded_shape == "auto" and shape["reduce_possible"]:
+            other = "gather" if shape["shape"] == "reduce" else "reduce"
+            out["other_shape"] = other_shape(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak, other)
     else:
         out["one_set"] = "at N = 1 the leg itself: one set on one GPU"
     return out
 
 
-def one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak):
-    """BASELINE.md's C4 word for word: ONE RS(8+3) set (configs[2]'s data)
-    column-sharded over the N GPUs -- strong scaling, member r on GPU r mod N,
-    every GPU rebuilding its 1/N column slice of every stripe. The same three
-    loops as the leg (the step, the decode on slices in place, the exchange
-    alone), K steps each, bracketed and max over ranks; bit-exact checked."""
+def runner_loops(runner, args, world, warm, reduce, link_peak):
+    """The leg's three loops on a runner whose lost members are erased: the
+    step (K rebuilds), the decode on slices in place (COMPUTE + ACCUMULATE)
+    and the exchange alone (GATHER + RETURN), K steps each, bracketed and max
+    over ranks; bit-exact checked after the step loop."""
     import torch
     import torch.distributed as dist
 
     import redset_amd
-    from redset_amd import dist as rdist
     from redset_amd._lib import PHASE_ACCUMULATE, PHASE_COMPUTE, PHASE_GATHER, PHASE_RETURN
 
-    runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, sets=1, shape=args.sharded_shape,
-                                    transport=args.sharded_transport or None)
-    shape = runner.shape("rebuild")
     runner.timing = False
     runner.encode()
     snap = runner.lost_snapshot()
@@ -613,17 +612,16 @@ def one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak):
                    min(warm, args.warmup), dist_on) / args.steps
     total = runner.total_algorithmic_bytes("rebuild")
     sent_mean = reduce(float(runner.exchanged_bytes("rebuild")), dist.ReduceOp.SUM, torch.float64) / world
+    shape = runner.shape("rebuild")
     torch.cuda.synchronize()
     runner.close()
     peak = world * HBM_PEAK_GBPS
     return {
-        "workload": (f"one set of p={p} (RS({p - e}+{e}), chunk {chunk / MIB:g} MiB) over {world} GPUs, member r on "
-                     f"GPU r mod {world}; rebuild of {lost} (BASELINE.md C4, strong scaling)"),
+        "shape": shape["shape"],
         "value": round(total / step / 1e9, 2),
         "frac_of_hbm": round(total / step / 1e9 / peak, 6),
         "ms_per_step": round(step * 1e3, 4),
         "bit_exact": bool(ok),
-        "shape": shape["shape"],
         "busiest_gpu_bytes_by_shape": {"gather": shape["gather_busiest_bytes"],
                                        "reduce": shape["reduce_busiest_bytes"] if shape["reduce_possible"] else None},
         "decode": {"value": round(total / d_step / 1e9, 2), "frac_of_hbm": round(total / d_step / 1e9 / peak, 6),
@@ -633,6 +631,34 @@ def one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak):
                           "send_GBps_per_gpu": round(sent_mean / x_step / 1e9, 2) if sent_mean else None,
                           "frac_of_xgmi": round(sent_mean / x_step / 1e9 / link_peak, 4) if sent_mean else None},
     }
+
+
+def one_set(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak):
+    """BASELINE.md's C4 word for word: ONE RS(8+3) set (configs[2]'s data)
+    column-sharded over the N GPUs -- strong scaling, member r on GPU r mod N,
+    every GPU rebuilding its 1/N column slice of every stripe. The same three
+    loops as the leg (the step, the decode on slices in place, the exchange
+    alone), K steps each, bracketed and max over ranks; bit-exact checked."""
+    from redset_amd import dist as rdist
+
+    runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, sets=1, shape=args.sharded_shape,
+                                    transport=args.sharded_transport or None)
+    out = {"workload": (f"one set of p={p} (RS({p - e}+{e}), chunk {chunk / MIB:g} MiB) over {world} GPUs, member r "
+                        f"on GPU r mod {world}; rebuild of {lost} (BASELINE.md C4, strong scaling)")}
+    out.update(runner_loops(runner, args, world, warm, reduce, link_peak))
+    return out
+
+
+def other_shape(args, p, e, chunk, lost, world, rank, warm, reduce, link_peak, shape):
+    """The leg once more with the exchange shape the planner did NOT take
+    (forced), the same three loops: the measured A/B behind the planner's
+    byte-count choice (gather = C4's column-sharded decode as BASELINE.md
+    states it; reduce = partial sums of each GPU's own inputs)."""
+    from redset_amd import dist as rdist
+
+    runner = rdist.ShardedSetRunner(p, e, chunk, lost, world=world, rank=rank, shape=("auto", shape),
+                                    transport=args.sharded_transport or None)
+    return runner_loops(runner, args, world, warm, reduce, link_peak)
 
 
 _PRINT_LOCK = threading.Lock()

@@ -84,6 +84,10 @@ def test_bench_two_ranks_self_launched_over_gloo():
     assert line["config"]["scaling_value_GBps"] == line["sharded"]["value"] == line["scaling_value_GBps"]
     cb = line["cpu_baseline"]
     assert cb["value"] > 0 and cb["kind"] == "port" and cb["cores"] >= 1, cb
+    # the shape the planner did not take, measured beside it, bit-exact
+    other = line["sharded"]["other_shape"]
+    assert other["bit_exact"] is True and other["shape"] != line["sharded"]["shape"], other
+    assert other["value"] > 0 and other["decode"]["value"] > 0, other
 
 
 @pytest.mark.timeout(420)

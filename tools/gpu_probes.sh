@@ -8,6 +8,9 @@
 #   rank   the per-rank slot's roofline (tools/rank_bench.py): RS(8+3) 64 MiB
 #          and configs[0] (XOR, 4 x 16 MiB files), host and sharded exchanges
 #          (RANK_EXCHANGES, default "host sharded-mpi sharded-host")
+#   slotbuf  the slot's RS(8+3) 64 MiB encode / rebuild over the host ring and the
+#          host slabs at the reference's default 1 MiB MPI buffer and at 16 MiB
+#          (round 6: the sharded window no longer grows with the buffer)
 #   wide   RS(16+4) (configs[4]'s stripe) device-resident: kernel stats, PMC
 #          FETCH/WRITE and SQ counters
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -42,6 +45,23 @@ for probe in "$@"; do
         run rank_config0_$ex 200 python tools/rank_bench.py --scheme xor --ranks 4 --file-bytes 16777216 \
           --buf-mib 1 --repeat 5 --exchange $ex --lost 2 --dir /tmp/rank_c0_$ex
       done ;;
+    slotbuf)
+      for buf in ${SLOT_BUFS:-1 16}; do
+        for ex in host sharded-host; do
+          run rank_rs_64m_${ex}_buf$buf 400 python tools/rank_bench.py --ranks 11 --encoding 3 --chunk-mib 64 \
+            --buf-mib $buf --repeat 5 --exchange $ex --dir /tmp/rank_bench_$ex
+        done
+      done ;;
+    slotwin)
+      # the host-slab encode at the default 1 MiB buffer with the test twin's
+      # window override: the window's effect alone (bytes per window per cell)
+      for win in ${SLOT_WINS:-4194304 8388608 16777216}; do
+        LD_LIBRARY_PATH=$PWD/redset_amd/lib_test${LD_LIBRARY_PATH:+:$LD_LIBRARY_PATH} REDSET_HIP_TEST_SHARDED_WINDOW=$win \
+          run rank_rs_64m_sharded-host_win$win 400 python tools/rank_bench.py --ranks 11 --encoding 3 --chunk-mib 64 \
+            --buf-mib 1 --repeat 5 --exchange sharded-host --dir /tmp/rank_bench_win
+      done
+      run rank_rs_64m_host_buf1_again 400 python tools/rank_bench.py --ranks 11 --encoding 3 --chunk-mib 64 \
+        --buf-mib 1 --repeat 5 --exchange host --dir /tmp/rank_bench_host ;;
     wide)
       W="--ranks 20 --encoding 4 --lost 1,2,3,4 --cpu-baseline 0 --pairs 0 --xor 0"
       run wide_bench 300 python bench.py --steps 10 --warmup 3 $W

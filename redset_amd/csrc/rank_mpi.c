@@ -1612,8 +1612,14 @@ static int slot_done(comm_exchange* X, slot_ctx* C, int rc) {
  * (d + e)(p - 1)/p cells for the encode, where the reference's ring sends
  * every data cell to each of the e parity holders, d*e cells
  * (src/redset_reedsolomon.c:329-363): RS(8+3) 10 cells instead of 24.
- * Windows alternate between two slab sets (SHARDED_WINDOW / 2 of cells each,
- * so both fit the window budget) and their phases overlap: window n's
+ * Windows alternate between two slab sets of SHARDED_WINDOW of cells each
+ * (a member's p cells; each set holds the hosted and the gathered slabs, so
+ * ~4 p win = 384 MiB pinned in all, whatever the MPI buffer: round 6 cut the
+ * window from the buffer size, which had pinned 2.8 GiB at a 64 MiB buffer
+ * (ADVICE r5), and measured the window at the default 1 MiB buffer, RS(8+3),
+ * 64 MiB chunks, one box: 4 / 8 / 16 MiB windows encode in 0.715 / 0.524 /
+ * 0.579 s against the host ring's 0.808 s, profiles/r06s5_*), and their
+ * phases overlap: window n's
  * kernels run on the GPU while the host writes window n - 1, reads window
  * n + 1 and runs its gather; window n's return follows. Every member runs the
  * same collectives in the same order: agree(n), gather(n), return(n - 1). */
@@ -1621,7 +1627,7 @@ static int sharded_slot_host(int encode, const redset_hip_rs* rs, MPI_Comm comm,
                              const int* lost, int need_rebuild, const redset_hip_io* lofi, const char* chunk_file,
                              int fd_chunk, off_t header, int hrc, size_t chunk_size, size_t B, comm_exchange* X) {
   const int d = p - e, ncell = p, world = p;
-  const size_t win = slot_window(SHARDED_WINDOW / 2, chunk_size, ncell, B);
+  const size_t win = slot_window(SHARDED_WINDOW, chunk_size, ncell, B);
   int rc = hrc;
   if (!rc && need_rebuild && !lofi->write) rc = fail("lofi has no write callback");
   int crc = 0;

@@ -8,6 +8,8 @@
 #   rank   the per-rank slot's roofline (tools/rank_bench.py): RS(8+3) 64 MiB
 #          and configs[0] (XOR, 4 x 16 MiB files), host and sharded exchanges
 #          (RANK_EXCHANGES, default "host sharded-mpi sharded-host")
+#   slotab the slot's RS(8+3) 64 MiB encode / rebuild, host ring vs host slabs at the
+#          default 1 MiB buffer, alternating, twice each
 #   slotbuf  the slot's RS(8+3) 64 MiB encode / rebuild over the host ring and the
 #          host slabs at the reference's default 1 MiB MPI buffer and at 16 MiB
 #          (round 6: the sharded window no longer grows with the buffer)
@@ -62,6 +64,15 @@ for probe in "$@"; do
       done
       run rank_rs_64m_host_buf1_again 400 python tools/rank_bench.py --ranks 11 --encoding 3 --chunk-mib 64 \
         --buf-mib 1 --repeat 5 --exchange host --dir /tmp/rank_bench_host ;;
+    slotab)
+      # host ring against host slabs at the default 1 MiB buffer, alternating
+      # (one box's shared-memory MPI drifts by +-20% between calls)
+      for rep in 1 2; do
+        for ex in host sharded-host; do
+          run rank_rs_64m_${ex}_ab$rep 400 python tools/rank_bench.py --ranks 11 --encoding 3 --chunk-mib 64 \
+            --buf-mib 1 --repeat 5 --exchange $ex --dir /tmp/rank_bench_$ex
+        done
+      done ;;
     wide)
       W="--ranks 20 --encoding 4 --lost 1,2,3,4 --cpu-baseline 0 --pairs 0 --xor 0"
       run wide_bench 300 python bench.py --steps 10 --warmup 3 $W

@@ -131,7 +131,8 @@ int redset_hip_rank_last_stats(redset_hip_rank_stats* out);
  * paths a few buffers of buf_size; the sharded exchanges two window images
  * of 96 MiB, plus, over the MPI transport (_SHARDED_MPI), a staging buffer of
  * one exchange's bytes sent and received (up to ~2 x 96 MiB); over host slabs
- * (_SHARDED_HOST) two slab sets of ~96 MiB and no device memory. The
+ * (_SHARDED_HOST) two slab sets of ~192 MiB (a 96 MiB window of the p cells,
+ * hosted and gathered: ~384 MiB) and no device memory. The
  * sharded windows are cut from these budgets whatever buf_size is (a window
  * never grows to the MPI buffer).
  * The host paths keep a successful call's pinned host buffers, device

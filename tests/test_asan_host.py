@@ -64,6 +64,25 @@ def test_sharded_planner_asan(asan_build, np_, args, idle):
     assert res.returncode == 0, res.stdout + res.stderr[-4000:]
 
 
+@pytest.mark.skipif(not os.path.exists(MPIRUN), reason="needs MPICH's mpirun")
+@pytest.mark.parametrize("np_", [2, 3, 4])
+@pytest.mark.parametrize("args", [(11, 3, 3001, 1, 2), (6, 2, 1, 0, 3), (5, 1, 65537, 4)])
+@pytest.mark.parametrize("shape", ["reduce", "auto"])
+def test_sharded_partial_sums_asan(asan_build, np_, args, shape):
+    """The partial-sum shape's planner (sharded.c ra_build / plan_reduce:
+    row allocation for every process, merged messages, combine job lists)
+    and its execute, under ASan + LeakSanitizer; a forced plan that does
+    not fit must fail cleanly (no leak on the error path)."""
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", os.path.join(asan_build, "sharded_test")] + \
+        [str(a) for a in args]
+    env = {**ENV, "SHARDED_TEST_SHAPE": shape}
+    if args[1] == 1:
+        env["SHARDED_TEST_SCHEME"] = "xor"
+    res = run_group(cmd, 180, env=env)
+    assert _clean(res), res.stderr[-4000:]
+    assert res.returncode == 0 or (shape == "reduce" and "do not fit" in res.stderr), res.stdout + res.stderr[-4000:]
+
+
 def _framed(path, text):
     fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
     H.write_header(fd, H.parse(text))

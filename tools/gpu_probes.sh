@@ -8,6 +8,8 @@
 #   rank   the per-rank slot's roofline (tools/rank_bench.py): RS(8+3) 64 MiB
 #          and configs[0] (XOR, 4 x 16 MiB files), host and sharded exchanges
 #          (RANK_EXCHANGES, default "host sharded-mpi sharded-host")
+#   stubn  bench.py --gpus 3 / 4 self-launched, sharded leg over the RCCL transport on
+#          the test stand-in (tests/rcclstub), 4 MiB chunks
 #   slotab the slot's RS(8+3) 64 MiB encode / rebuild, host ring vs host slabs at the
 #          default 1 MiB buffer, alternating, twice each
 #   slotbuf  the slot's RS(8+3) 64 MiB encode / rebuild over the host ring and the
@@ -72,6 +74,17 @@ for probe in "$@"; do
           run rank_rs_64m_${ex}_ab$rep 400 python tools/rank_bench.py --ranks 11 --encoding 3 --chunk-mib 64 \
             --buf-mib 1 --repeat 5 --exchange $ex --dir /tmp/rank_bench_$ex
         done
+      done ;;
+    stubn)
+      # the bench's self-launched N = 3 / 4 flow with the sharded leg over the
+      # RCCL transport (test twin + tests/rcclstub: any number of ranks per
+      # GPU), 4 MiB chunks: AUTO's shape, the shape not taken, one set over N
+      for n in ${STUB_NS:-3 4}; do
+        REDSET_HIP_LIBRARY=$PWD/redset_amd/lib_test/libredset_hip.so \
+          REDSET_HIP_TEST_RCCL_LIBRARY=$PWD/tests/rcclstub/lib/librccl.so.1 \
+          run bench_stub_n$n 500 python bench.py --gpus $n --dist-backend gloo --sharded-transport rccl \
+            --chunk-mib 4 --steps 3 --warmup 1 --cpu-baseline 1 --cpu-seconds 1 --pairs 0 --xor 0 \
+            --sharded-timeout 300
       done ;;
     wide)
       W="--ranks 20 --encoding 4 --lost 1,2,3,4 --cpu-baseline 0 --pairs 0 --xor 0"

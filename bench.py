@@ -139,8 +139,11 @@ def cpu_baseline(p, e, lost, target_s, chunk):
     reb_bytes = p * (d + len(lost)) * chunk * passes
     # (ii) of SURVEY.md §8d: one thread of redset_rs_reduce_buffer_multadd's
     # premult loop (src/redset_reedsolomon_common.c:798-811) on 64 MiB slices
-    buf = np.zeros(64 * MIB, np.uint8)
-    src = np.ascontiguousarray(lofi[0][:64 * MIB])
+    # (the source is the first member's logical file, d cells: at small
+    # chunks shorter than 64 MiB, and multadd reads buf.size bytes of it)
+    n_ma = min(64 * MIB, lofi[0].size)
+    buf = np.zeros(n_ma, np.uint8)
+    src = np.ascontiguousarray(lofi[0][:n_ma])
     reps, t_ma = 0, 0.0
     while t_ma < min(3.0, target_s / 3):
         t0 = time.perf_counter()
@@ -163,7 +166,7 @@ def cpu_baseline(p, e, lost, target_s, chunk):
         "host_cpus": os.cpu_count(),
         "cpu_model": _cpu_model(),
         # input bytes of one multadd (data read; the accumulator's RMW not counted), GB/s
-        "multadd_1thread_GBps": round(reps * 64 * MIB / t_ma / 1e9, 4),
+        "multadd_1thread_GBps": round(reps * n_ma / t_ma / 1e9, 4),
     }
 
 

@@ -106,6 +106,8 @@ class OracleRS:
         return self.L.ro_rs_get_data_id(self.ranks, self.encoding, rank, chunk)
 
     def multadd(self, buf: np.ndarray, coeff: int, data: np.ndarray):
+        if data.size < buf.size:
+            raise ValueError(f"multadd: {data.size} B of data for {buf.size} B of buffer")
         self.L.ro_rs_multadd(self.h, buf.size, buf.ctypes.data, coeff, data.ctypes.data)
 
     def encode_set(self, lofi, parity, chunk_size: int, slice_bytes: int = 1 << 20):

@@ -31,6 +31,8 @@ int hipMalloc(void** p, size_t n) { *p = malloc(n ? n : 1); return *p ? 0 : 2; }
 int hipFree(void* p) { free(p); return 0; }
 int hipMemcpyAsync(void* d, const void* s, size_t n, int k, void* st) { (void) k; (void) st; memmove(d, s, n); return 0; }
 int hipMemcpy(void* d, const void* s, size_t n, int k) { (void) k; memmove(d, s, n); return 0; }
+int hipMemset(void* d, int v, size_t n) { memset(d, v, n); return 0; }
+int hipMemsetAsync(void* d, int v, size_t n, void* st) { (void) st; memset(d, v, n); return 0; }
 int hipMemcpy2DAsync(void* d, size_t dp, const void* s, size_t sp, size_t w, size_t h, int k, void* st) {
   (void) k; (void) st;
   for (size_t i = 0; i < h; ++i) memmove((char*) d + i * dp, (const char*) s + i * sp, w);
@@ -108,9 +110,18 @@ int redset_hip_rs_get_data_id(int ranks, int encoding, int rank, int chunk_id);
 int redset_hip_rs_decode_matrix(const redset_hip_rs* rs, int missing, const int* rebuild_ranks, int chunk_id,
                                 unsigned char* coef_out);
 
-enum { STUB_RS_ENCODE = 1, STUB_RS_REBUILD = 2, STUB_XOR_ENCODE = 3, STUB_XOR_REBUILD = 4 };
+enum { STUB_RS_ENCODE = 1, STUB_RS_REBUILD = 2, STUB_XOR_ENCODE = 3, STUB_XOR_REBUILD = 4, STUB_COMBINE = 5 };
+/* a combine plan's job (include/redset_hip.h redset_hip_combine_job), copied */
+typedef struct {
+  int nin, nout, acc;
+  const unsigned char** in;
+  unsigned char** out;
+  unsigned char* coef;
+} stub_job;
 struct redset_hip_plan {
   int kind, p, e, missing, lost[256];
+  stub_job* jobs; /* STUB_COMBINE */
+  int njobs;
   /* the coefficients, copied at plan time as the library's plans do (the
    * caller may destroy its codec while the plan lives): the encoding matrix,
    * or every stripe's decode map */
@@ -161,8 +172,45 @@ int redset_hip_xor_plan_rebuild(int p, int root, unsigned char* const* lofi, uns
                                 size_t chunk, size_t stride, struct redset_hip_plan** out) {
   return stub_plan(STUB_XOR_REBUILD, NULL, p, 1, 1, &root, lofi, xorc, chunk, stride, out);
 }
+/* redset_hip_plan_combine on the CPU: the sharded plans' partial-sum shape
+ * builds its combines through it (sharded.c plan_reduce); execute runs them
+ * with the stand-in gf_combine above */
+typedef struct {
+  int nin, nout;
+  const unsigned char* const* in;
+  unsigned char* const* out;
+  const unsigned char* coef;
+  int accumulate;
+} stub_combine_job;
+int redset_hip_plan_combine(const stub_combine_job* jobs, int njobs, size_t nbytes, struct redset_hip_plan** out) {
+  struct redset_hip_plan* P = calloc(1, sizeof(*P));
+  if (!P) return 1;
+  P->kind = STUB_COMBINE;
+  P->n = nbytes;
+  P->jobs = calloc((size_t) (njobs > 0 ? njobs : 1), sizeof(stub_job));
+  P->njobs = njobs;
+  for (int k = 0; k < njobs; ++k) {
+    stub_job* J = &P->jobs[k];
+    J->nin = jobs[k].nin, J->nout = jobs[k].nout, J->acc = jobs[k].accumulate;
+    J->in = malloc(sizeof(*J->in) * (size_t) J->nin);
+    J->out = malloc(sizeof(*J->out) * (size_t) J->nout);
+    J->coef = malloc((size_t) J->nin * (size_t) J->nout);
+    memcpy(J->in, jobs[k].in, sizeof(*J->in) * (size_t) J->nin);
+    memcpy(J->out, jobs[k].out, sizeof(*J->out) * (size_t) J->nout);
+    memcpy(J->coef, jobs[k].coef, (size_t) J->nin * (size_t) J->nout);
+  }
+  *out = P;
+  return 0;
+}
+
 void redset_hip_plan_destroy(struct redset_hip_plan* P) {
   if (!P) return;
+  for (int k = 0; k < P->njobs; ++k) {
+    free(P->jobs[k].in);
+    free(P->jobs[k].out);
+    free(P->jobs[k].coef);
+  }
+  free(P->jobs);
   free(P->coef);
   free(P->lofi);
   free(P->par);
@@ -180,6 +228,13 @@ static unsigned char* stub_cell(const struct redset_hip_plan* P, int r, int c) {
 
 int redset_hip_plan_execute(const struct redset_hip_plan* P, void* stream) {
   (void) stream;
+  if (P->kind == STUB_COMBINE) {
+    for (int k = 0; k < P->njobs; ++k) {
+      const stub_job* J = &P->jobs[k];
+      redset_hip_gf_combine(J->in, J->nin, J->out, J->nout, J->coef, P->n, J->acc, stream);
+    }
+    return 0;
+  }
   const int p = P->p, e = P->e;
   const unsigned char* mat = P->coef;
   for (int c = 0; c < p; ++c) {

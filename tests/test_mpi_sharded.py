@@ -346,3 +346,34 @@ def test_rccl_transport_at_world_above_one_on_cpu(oracle, shape, scheme, np_, p,
     assert res.returncode == 0, res.stdout + res.stderr
     assert res.stdout.count("rebuild gather") == np_
     assert not [f for f in os.listdir("/dev/shm") if f.startswith("rcclstub_")], "stand-in left shared memory"
+
+
+@pytest.mark.parametrize("transport", ["mpi", "rccl"])
+@pytest.mark.parametrize("shape", ["gather", "reduce", "auto"])
+@pytest.mark.parametrize("mode", ["--gpu", "--gpu-host"])
+@pytest.mark.parametrize("scheme,np_,p,e,chunk,lost", [("rs", 3, 11, 3, 30001, [1, 2]), ("rs", 2, 20, 4, 4097, [0, 5, 19]),
+                                                        ("xor", 3, 8, 1, 3001, [3])])
+def test_hip_plan_paths_on_cpu(oracle, transport, shape, mode, scheme, np_, p, e, chunk, lost):
+    """sharded_test's HIP modes with tests/mpi/hipstub.c standing in for the
+    runtime and the plans (the set plans and, round 6, redset_hip_plan_combine):
+    the pipelined executes of both shapes -- the plan's exchange stream and
+    events, set k's exchange after its compute, the partial sums' accumulate
+    after its exchange -- over the MPI transport with device staging (--gpu)
+    or host slabs, and over the RCCL transport (tests/rcclstub), against the
+    oracle. The GPU suite runs the same with the real kernels."""
+    if not _have() or not os.path.exists(HIPSTUB) or not os.path.exists(os.path.join(RCCLSTUB_DIR, "librccl.so.1")):
+        pytest.skip("needs MPICH, tests/mpi/build/libhipstub.so and tests/rcclstub")
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", "-genv", "LD_PRELOAD", HIPSTUB, DRIVER, mode, str(p), str(e),
+           str(chunk)] + [str(x) for x in lost]
+    ld = os.environ.get("LD_LIBRARY_PATH")
+    env = {**os.environ, "SHARDED_TEST_TRANSPORT": transport, "SHARDED_TEST_SHAPE": shape,
+           "LD_LIBRARY_PATH": RCCLSTUB_DIR + (":" + ld if ld else "")}
+    if scheme == "xor":
+        env["SHARDED_TEST_SCHEME"] = "xor"
+    res = run_group(cmd, 120, env=env, cwd="/tmp")
+    if res.returncode != 0 and shape == "reduce" and "do not fit" in res.stderr:
+        pytest.skip("the partial sums do not fit this placement's scratch")
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert res.stdout.count("rebuild gather") == np_
+    if shape != "auto":
+        assert res.stdout.count(f"rebuild shape {shape}") == np_, res.stdout

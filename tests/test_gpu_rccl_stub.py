@@ -32,7 +32,8 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 STUB_DIR = os.path.join(ROOT, "tests", "rcclstub", "lib")
 STUB = os.path.join(STUB_DIR, "librccl.so.1")
 TWIN = os.path.join(ROOT, "redset_amd", "lib_test", "libredset_hip.so")
-DRIVER = os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
+# SHARDED_TEST_BIN: another build of the driver (tools/gpu_asan.sh: host ASan)
+DRIVER = os.environ.get("SHARDED_TEST_BIN") or os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
 
 
 def _stub_env(extra=None):

@@ -16,7 +16,9 @@ export ASAN_OPTIONS="verify_asan_link_order=0:detect_leaks=${DETECT_LEAKS:-0}:ex
 export LSAN_OPTIONS="suppressions=$PWD/tests/asan/lsan.supp"
 export REDSET_HIP_REBUILD_TOOL=$PWD/$B/redset_hip_rebuild RANK_TEST_BIN=$PWD/$B/rank_test SHARDED_TEST_BIN=$PWD/$B/sharded_test
 timeout -k 10 600 python -u -m pytest -x -v --timeout 100 --timeout-method thread \
-  tests/test_gpu_rebuild_tool.py tests/test_gpu_mpi.py > "$OUT/asan_tests.log" 2>&1
+  tests/test_gpu_rebuild_tool.py tests/test_gpu_mpi.py "tests/test_gpu_rccl_stub.py::test_sharded_rccl_transport_with_hip_kernels" \
+  "tests/test_gpu_rccl_stub.py::test_sharded_reduce_shape_over_mpi" "tests/test_gpu_rccl_stub.py::test_rank_backends_forced_rccl" \
+  > "$OUT/asan_tests.log" 2>&1
 s=$?
 tail -5 "$OUT/asan_tests.log"
 grep -c "AddressSanitizer\|LeakSanitizer" "$OUT/asan_tests.log" || true

@@ -18,6 +18,7 @@
  * receives every survivor's every cell, with slices gathered onto every GPU.
  */
 #include <hip/hip_runtime_api.h>
+#include <limits.h>
 #include <stdarg.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -484,8 +485,10 @@ typedef struct {
   unsigned char* coef;
   int* ord;                 /* [nsets][nout] set k's outputs by (pass, slot, cell) */
   uint64_t* mask;           /* [nsets][nout] contributing processes */
-  long* srow;               /* [k][o][q][g] row of sender g's scratch, or -1 */
-  long* rrow;               /* [k][o][q][g] row of the receiver's scratch, -1 (direct) */
+  int* srow;                /* [k][o][q][g] row of sender g's scratch, or -1 */
+  int* rrow;                /* [k][o][q][g] row of the receiver's scratch, -1 (direct) */
+  int* byhost;              /* [nsets][nout] set k's outputs in `ord` order, grouped by host */
+  int* hoff;                /* [nsets][world + 1] host h's outputs: byhost[hoff[h] .. hoff[h + 1]) */
   long *S, *R;              /* [world] scratch rows sent / received into scratch */
   unsigned long long *sent, *recvd; /* [world] rows sent / received */
   long rows;                /* scratch rows per process (the gathered slabs) */
@@ -496,6 +499,8 @@ static void ra_free(reduce_alloc* A) {
   free(A->oc);
   free(A->coef);
   free(A->ord);
+  free(A->byhost);
+  free(A->hoff);
   free(A->mask);
   free(A->srow);
   free(A->rrow);
@@ -515,6 +520,9 @@ static int ra_slot(const reduce_alloc* A, int k, int o) { return A->slot[(size_t
 static uint64_t ra_remote(const reduce_alloc* A, int k, int o) {
   return A->mask[(size_t) k * A->nout + o] & ~((uint64_t) 1 << ra_host(A, k, o));
 }
+
+/* where host h's outputs start among set k's outputs grouped by host */
+static int ra_lo(const reduce_alloc* A, int k, int h) { return A->hoff[(size_t) k * (size_t) (A->world + 1) + (size_t) h]; }
 
 /* set k's outputs by (pass, the host's slot, cell): the order of a pair's rows */
 static int ra_before(const reduce_alloc* A, int k, int oa, int ob) {
@@ -551,16 +559,19 @@ static int ra_build(reduce_alloc* A, const redset_hip_rs* rs, int p, int e, int 
     if ((size_t) q * A->W < A->C) A->nslices = q + 1;
   if (set_outputs(rs, p, e, kind, missing, lost, &A->oc, &A->coef, &A->nout)) return REDSET_FAILURE;
   const size_t nk = (size_t) A->nsets * A->nout, nkey = nk * (size_t) world * (size_t) world;
-  if (nkey > ((size_t) 1 << 26)) return 0; /* too many rows to plan this way */
+  if (nkey > ((size_t) 1 << 23)) return 0; /* too many rows to plan this way */
   A->ord = malloc(sizeof(int) * nk);
+  A->byhost = malloc(sizeof(int) * nk);
+  A->hoff = calloc((size_t) A->nsets * (size_t) (world + 1), sizeof(int));
   A->mask = calloc(nk, sizeof(uint64_t));
-  A->srow = malloc(sizeof(long) * nkey);
-  A->rrow = malloc(sizeof(long) * nkey);
+  A->srow = malloc(sizeof(int) * nkey);
+  A->rrow = malloc(sizeof(int) * nkey);
   A->S = calloc((size_t) world, sizeof(long));
   A->R = calloc((size_t) world, sizeof(long));
   A->sent = calloc((size_t) world, sizeof(unsigned long long));
   A->recvd = calloc((size_t) world, sizeof(unsigned long long));
-  if (!A->ord || !A->mask || !A->srow || !A->rrow || !A->S || !A->R || !A->sent || !A->recvd)
+  if (!A->ord || !A->byhost || !A->hoff || !A->mask || !A->srow || !A->rrow || !A->S || !A->R || !A->sent ||
+      !A->recvd)
     return sfail("out of host memory");
   for (size_t i = 0; i < nkey; ++i) A->srow[i] = A->rrow[i] = -1;
   A->ok = 1;
@@ -574,14 +585,24 @@ static int ra_build(reduce_alloc* A, const redset_hip_rs* rs, int p, int e, int 
       A->ord[(size_t) k * A->nout + o] = o;
     }
     ra_sort(A, k, A->ord + (size_t) k * A->nout, A->nout);
+    /* the sorted outputs bucketed by host, order kept */
+    int* off = A->hoff + (size_t) k * (size_t) (world + 1);
+    for (int o = 0; o < A->nout; ++o) ++off[ra_host(A, k, o) + 1];
+    for (int h = 0; h < world; ++h) off[h + 1] += off[h];
+    int* fill = calloc((size_t) world, sizeof(int));
+    if (!fill) return sfail("out of host memory");
+    for (int i = 0; i < A->nout; ++i) {
+      const int o = A->ord[(size_t) k * A->nout + i], h = ra_host(A, k, o);
+      A->byhost[(size_t) k * A->nout + (size_t) (off[h] + fill[h]++)] = o;
+    }
+    free(fill);
   }
   /* sender g's rows, in the order (set, receiver, slice, output) */
   for (int k = 0; k < A->nsets; ++k)
     for (int h = 0; h < world; ++h)
       for (int q = 0; q < A->nslices; ++q)
-        for (int i = 0; i < A->nout; ++i) {
-          const int o = A->ord[(size_t) k * A->nout + i];
-          if (ra_host(A, k, o) != h) continue;
+        for (int i = ra_lo(A, k, h); i < ra_lo(A, k, h + 1); ++i) {
+          const int o = A->byhost[(size_t) k * A->nout + i];
           const uint64_t rem = ra_remote(A, k, o);
           for (int g = 0; g < world; ++g)
             if (rem >> g & 1) {
@@ -593,29 +614,21 @@ static int ra_build(reduce_alloc* A, const redset_hip_rs* rs, int p, int e, int 
   /* receiver h's scratch rows (after its sent ones), in the order (set,
    * sender, slice, output); the first remote contributor's go straight in
    * the output */
-  for (int k = 0; k < A->nsets; ++k)
+  A->rows = (long) world * A->mh * (A->d + A->e);
+  for (int g = 0; g < world; ++g)
+    if (A->S[g] > A->rows || A->S[g] > INT_MAX / 2) A->ok = 0;
+  for (int k = 0; k < A->nsets && A->ok; ++k)
     for (int h = 0; h < world; ++h)
       for (int g = 0; g < world; ++g)
         for (int q = 0; q < A->nslices; ++q)
-          for (int i = 0; i < A->nout; ++i) {
-            const int o = A->ord[(size_t) k * A->nout + i];
-            if (ra_host(A, k, o) != h) continue;
+          for (int i = ra_lo(A, k, h); i < ra_lo(A, k, h + 1); ++i) {
+            const int o = A->byhost[(size_t) k * A->nout + i];
             const uint64_t rem = ra_remote(A, k, o);
             if (!(rem >> g & 1) || (rem & (~rem + 1)) == ((uint64_t) 1 << g)) continue;
-            A->rrow[ra_key(A, k, o, q, g)] = A->R[h]++;
+            A->rrow[ra_key(A, k, o, q, g)] = (int) (A->S[h] + A->R[h]++);
           }
-  A->rows = (long) world * A->mh * (A->d + A->e);
-  for (int g = 0; g < world; ++g) {
-    for (int k = 0; k < A->nsets; ++k) /* receiver rows start after the sent ones */
-      for (int o = 0; o < A->nout; ++o)
-        if (ra_host(A, k, o) == g)
-          for (int q = 0; q < A->nslices; ++q)
-            for (int s = 0; s < world; ++s) {
-              long* r = &A->rrow[ra_key(A, k, o, q, s)];
-              if (*r >= 0) *r += A->S[g];
-            }
+  for (int g = 0; g < world; ++g)
     if (A->S[g] + A->R[g] > A->rows) A->ok = 0;
-  }
   return 0;
 }
 
@@ -626,7 +639,7 @@ typedef struct {
   size_t off;
 } rloc;
 
-static rloc ra_scratch(const reduce_alloc* A, long row) {
+static rloc ra_scratch(const reduce_alloc* A, long row) {  /* row >= 0 */
   const long nD = (long) A->world * A->mh * A->d;
   rloc l = {row < nD ? 2 : 3, (size_t) (row < nD ? row : row - nD) * A->W};
   return l;
@@ -639,7 +652,7 @@ static rloc ra_output(const reduce_alloc* A, int k, int o, int q) {
 }
 /* where sender g's row of (k, o, q) lands at the receiver */
 static rloc ra_dest(const reduce_alloc* A, int k, int o, int q, int g) {
-  const long r = A->rrow[ra_key(A, k, o, q, g)];
+  const int r = A->rrow[ra_key(A, k, o, q, g)];
   return r < 0 ? ra_output(A, k, o, q) : ra_scratch(A, r);
 }
 
@@ -666,9 +679,9 @@ static int ra_messages(const reduce_alloc* A, const redset_hip_shard_layout* L, 
   rloc s0 = {0, 0}, r0 = {0, 0};
   size_t len = 0;
   for (int q = 0; q < A->nslices; ++q)
-    for (int i = 0; i < A->nout; ++i) {
-      const int o = A->ord[(size_t) k * A->nout + i];
-      if (ra_host(A, k, o) != h || !(ra_remote(A, k, o) >> g & 1)) continue;
+    for (int i = ra_lo(A, k, h); i < ra_lo(A, k, h + 1); ++i) {
+      const int o = A->byhost[(size_t) k * A->nout + i];
+      if (!(ra_remote(A, k, o) >> g & 1)) continue;
       const rloc sl = ra_scratch(A, A->srow[ra_key(A, k, o, q, g)]), rl = ra_dest(A, k, o, q, g);
       if (have && sl.buf == s0.buf && sl.off == s0.off + len && rl.buf == r0.buf && rl.off == r0.off + len) {
         len += A->W;
@@ -741,7 +754,7 @@ static int plan_reduce(redset_hip_sharded* P, const reduce_alloc* A, const redse
             const int extra0 = nin;
             for (int a = 0; grp == 1 && a < ns; ++a)
               for (int g = 0; g < world; ++g) {
-                const long r = A->rrow[ra_key(A, k, sel[a], q, g)];
+                const int r = A->rrow[ra_key(A, k, sel[a], q, g)];
                 if (ra_remote(A, k, sel[a]) >> g & 1 && r >= 0) ip[nin++] = ra_ptr(L, ra_scratch(A, r));
               }
             if (nin == 0) {
@@ -790,30 +803,44 @@ static int plan_reduce(redset_hip_sharded* P, const reduce_alloc* A, const redse
   return rc;
 }
 
-/* the gather shape's bytes sent / received by process `who` (the planner's
- * own lists, merged as it merges them) */
-static int gather_counts(const pctx* C0, int who, unsigned long long* sent, unsigned long long* recvd) {
-  pctx C = *C0;
-  C.me = who;
-  C.me_s = C.sidx[who];
-  *sent = *recvd = 0;
-  int rc = 0;
-  for (int k = 0; k < C.L->nsets && !rc; ++k) {
-    exch G, R;
-    rc = ex_init(&G, C.world, who);
-    if (!rc) rc = ex_init(&R, C.world, who);
-    if (!rc) rc = plan_gather(&C, k, &G);
-    if (!rc) rc = plan_return(&C, k, &R);
-    for (int g = 0; g < C.world && !rc; ++g) {
-      for (int i = 0; i < G.send[g].n; ++i) *sent += G.send[g].v[i].len;
-      for (int i = 0; i < R.send[g].n; ++i) *sent += R.send[g].v[i].len;
-      for (int i = 0; i < G.recv[g].n; ++i) *recvd += G.recv[g].v[i].len;
-      for (int i = 0; i < R.recv[g].n; ++i) *recvd += R.recv[g].v[i].len;
-    }
-    ex_free(&G);
-    ex_free(&R);
+/* the gather shape's bytes sent / received by every process, from the
+ * placement alone (the planner's lists carry the same totals; merging rows
+ * into messages does not change them): every wanted cell of a member goes,
+ * one W-byte slice each, to every computing process but its host, and every
+ * output cell of a member comes back from every computing process but its
+ * host. O(members x processes), so AUTO can weigh every process's counts
+ * at any world size */
+static int gather_counts_all(const pctx* C, unsigned long long* sent, unsigned long long* recvd) {
+  const int p = C->p, world = C->world;
+  int* wc = calloc((size_t) p, sizeof(int)); /* member r's wanted cells */
+  if (!wc) return sfail("out of host memory");
+  for (int r = 0; r < p; ++r) {
+    for (int x = 0; x < C->d; ++x) wc[r] += wanted(C, r, 0, x);
+    for (int x = 0; x < C->e; ++x) wc[r] += wanted(C, r, 1, x);
   }
-  return rc;
+  int K = 0;
+  for (int g = 0; g < world; ++g) K += C->sidx[g] >= 0;
+  memset(sent, 0, sizeof(*sent) * (size_t) world);
+  memset(recvd, 0, sizeof(*recvd) * (size_t) world);
+  const unsigned long long W = C->W;
+  for (int k = 0; k < C->L->nsets; ++k)
+    for (int r = 0; r < p; ++r) {
+      const int h = C->L->host[(size_t) k * p + r], hc = C->sidx[h] >= 0;
+      /* the gather: my wanted cells to every other computing process */
+      sent[h] += (unsigned long long) wc[r] * W * (unsigned long long) (K - hc);
+      for (int g = 0; g < world && wc[r]; ++g)
+        if (g != h && C->sidx[g] >= 0) recvd[g] += (unsigned long long) wc[r] * W;
+      /* the return: an output member's cells from every other computing process */
+      int is_out = is_encode(C->kind);
+      for (int i = 0; i < C->missing; ++i) is_out |= C->lost[i] == r;
+      if (!is_out) continue;
+      const unsigned long long len = (unsigned long long) (is_encode(C->kind) ? C->e : C->d + C->e) * W;
+      recvd[h] += len * (unsigned long long) (K - hc);
+      for (int g = 0; g < world; ++g)
+        if (g != h && C->sidx[g] >= 0) sent[g] += len;
+    }
+  free(wc);
+  return 0;
 }
 
 /* what the _ex entry points pass down; the legacy ones plan GATHER and
@@ -918,14 +945,14 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
    * the one whose busiest process moves fewer bytes */
   if (want && want->compare) {
     redset_hip_sharded_shape_info* S = &P->shape_info;
+    unsigned long long* gs = calloc((size_t) world * 2, sizeof(unsigned long long));
+    rc = gs ? gather_counts_all(&C, gs, gs + world) : sfail("out of host memory");
     for (int g = 0; g < world && !rc; ++g) {
-      if (world > REDUCE_MAX_WORLD && g != me) continue; /* wide worlds: my own counts only */
-      unsigned long long sn = 0, rv = 0;
-      rc = gather_counts(&C, g, &sn, &rv);
-      const unsigned long long b = sn > rv ? sn : rv;
+      const unsigned long long b = gs[g] > gs[world + g] ? gs[g] : gs[world + g];
       if (b > S->gather_busiest_bytes) S->gather_busiest_bytes = b;
-      if (g == me) S->gather_bytes_sent = sn, S->gather_bytes_recv = rv;
     }
+    if (!rc) S->gather_bytes_sent = gs[me], S->gather_bytes_recv = gs[world + me];
+    free(gs);
     /* the partial sums need every process computing, and either the HIP
      * plans or a combine callback (a whole-set callback cannot run them) */
     const int can = !compute && (!comp || !comp->run || want->combine);

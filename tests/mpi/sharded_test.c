@@ -297,6 +297,20 @@ int main(int argc, char** argv) {
            me, i == 0 ? "encode" : "rebuild", shape_name(si.shape), shape_name(opts.shape), si.gather_busiest_bytes,
            si.reduce_busiest_bytes, si.reduce_possible, si.gather_bytes_sent, si.reduce_bytes_sent,
            si.scratch_bytes_needed, si.scratch_bytes);
+    /* the shape counts (computed from the placement) against the planned
+     * lists' own totals */
+    redset_hip_sharded_info inf;
+    if (redset_hip_sharded_get_info(pl, &inf) == 0) {
+      const unsigned long long ls = inf.gather_bytes_sent + inf.return_bytes_sent;
+      const unsigned long long lr = inf.gather_bytes_recv + inf.return_bytes_recv;
+      const unsigned long long ws = si.shape == REDSET_HIP_SHAPE_REDUCE ? si.reduce_bytes_sent : si.gather_bytes_sent;
+      const unsigned long long wr = si.shape == REDSET_HIP_SHAPE_REDUCE ? si.reduce_bytes_recv : si.gather_bytes_recv;
+      if (ls != ws || lr != wr) {
+        fprintf(stderr, "rank %d: %s: the shape info counts %llu / %llu B, the plan's lists %llu / %llu B\n", me,
+                i == 0 ? "encode" : "rebuild", ws, wr, ls, lr);
+        ok = 0;
+      }
+    }
   }
   int bad = 0;
   if (ok && redset_hip_sharded_execute(enc, stream) != 0) {

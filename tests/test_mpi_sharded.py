@@ -68,7 +68,8 @@ def test_sharded_plan_random_shapes_and_placements(oracle, seed):
 @pytest.mark.parametrize("scheme,np_,p,e,chunk,lost,idle", [
     ("rs", 4, 11, 3, 3001, [1, 2], "1"), ("rs", 4, 11, 3, 4096, [1, 2], "0,2"), ("rs", 3, 6, 2, 1000, [0, 4], "2"),
     ("rs", 4, 20, 4, 777, [0, 5, 19], "3"), ("rs", 2, 6, 3, 1, [2], "0"), ("xor", 4, 5, 1, 999, [3], "1,3")])
-def test_sharded_plan_with_idle_processes(oracle, scheme, np_, p, e, chunk, lost, idle):
+@pytest.mark.parametrize("shape", ["", "auto"])
+def test_sharded_plan_with_idle_processes(oracle, scheme, np_, p, e, chunk, lost, idle, shape):
     """redset_hip_{rs,xor}_sharded_plan_on: some processes compute no column
     slice (the slot's host-slab decode keeps its lost members out of the
     compute), the others take slices 0 .. K - 1 of ceil(C / K); every process
@@ -81,9 +82,15 @@ def test_sharded_plan_with_idle_processes(oracle, scheme, np_, p, e, chunk, lost
     env = {**os.environ, "SHARDED_TEST_IDLE": idle}
     if scheme == "xor":
         env["SHARDED_TEST_SCHEME"] = "xor"
+    if shape:
+        # through the _ex entry point: a compute mask keeps the gather shape,
+        # and the driver checks the shape info's byte counts against the lists
+        env["SHARDED_TEST_SHAPE"] = shape
     res = run_group(cmd, 120, env=env, cwd="/tmp")
     assert res.returncode == 0, res.stdout + res.stderr
     assert res.stdout.count("rebuild gather") == np_
+    if shape:
+        assert res.stdout.count("rebuild shape gather") == np_, res.stdout
 
 
 @pytest.mark.parametrize("np_,p,chunk,root", [

@@ -10,6 +10,8 @@
 #          (RANK_EXCHANGES, default "host sharded-mpi sharded-host")
 #   stubn  bench.py --gpus 3 / 4 self-launched, sharded leg over the RCCL transport on
 #          the test stand-in (tests/rcclstub), 4 MiB chunks
+#   stubfull bench.py --gpus 2 at 64 MiB chunks over the RCCL stand-in: both shapes'
+#          decode loops on the real kernels
 #   slotab the slot's RS(8+3) 64 MiB encode / rebuild, host ring vs host slabs at the
 #          default 1 MiB buffer, alternating, twice each
 #   slotbuf  the slot's RS(8+3) 64 MiB encode / rebuild over the host ring and the
@@ -86,6 +88,16 @@ for probe in "$@"; do
             --chunk-mib 4 --steps 3 --warmup 1 --cpu-baseline 1 --cpu-seconds 1 --pairs 0 --xor 0 \
             --sharded-timeout 300
       done ;;
+    stubfull)
+      # the bench's N = 2 sharded leg at full size (64 MiB chunks) over the
+      # RCCL stand-in: the step's rate is the stand-in's (shared-memory
+      # copies), but the decode loops (COMPUTE + ACCUMULATE, no exchange) run
+      # the real kernels of both shapes: the partial sums' combine plans
+      # against the gather shape's gf_mac plans (two ranks sharing one GPU)
+      REDSET_HIP_LIBRARY=$PWD/redset_amd/lib_test/libredset_hip.so \
+        REDSET_HIP_TEST_RCCL_LIBRARY=$PWD/tests/rcclstub/lib/librccl.so.1 \
+        run bench_stub_full_n2 900 python bench.py --gpus 2 --dist-backend gloo --sharded-transport rccl \
+          --steps 3 --warmup 1 --cpu-baseline 0 --pairs 0 --xor 0 --sharded-timeout 800 ;;
     wide)
       W="--ranks 20 --encoding 4 --lost 1,2,3,4 --cpu-baseline 0 --pairs 0 --xor 0"
       run wide_bench 300 python bench.py --steps 10 --warmup 3 $W

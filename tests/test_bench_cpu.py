@@ -12,7 +12,7 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-@pytest.mark.parametrize("chunk", [1 << 20, 4 << 20])
+@pytest.mark.parametrize("chunk", [1 << 20])
 def test_cpu_baseline_small_chunks(oracle, chunk):
     sys.path.insert(0, ROOT)
     import bench

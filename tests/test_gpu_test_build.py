@@ -31,15 +31,15 @@ on a healthy GPU:
 Two child runs of the suite, each in one process:
 1. the kernel-facing GPU tests (TWIN_FILES: every plan order, stripe width
    and cell size against the oracle, the streaming pipeline, full-size
-   digests, the hang contract, the doc examples, the HIP sharded compute and
-   the offline tool) with a 4-poll cap and a claimer delay: every test
+   digests and the hang contract) with a 4-poll cap and a claimer delay: every test
    compares bytes with the oracle or the golden digests, so a fallback that
    dropped or misplaced a byte fails that test; the child reports how many
    capped spins it counted (must be many) and which codec library it mapped.
-   The mpirun matrices (per-rank backends, adapter, RCCL stand-in) run the
-   same kernels through the same plans, and the twin changes none of their
-   host code, so they are not rerun (round 6: the rerun took 256 s of the
-   GPU suite's 598, VERDICT r5 item 2);
+   The mpirun matrices (per-rank backends, adapter, RCCL stand-in), the doc
+   examples, the sharded compute over gloo and the offline tool run the same
+   kernels through the same plans, and the twin changes none of their host
+   code, so they are not rerun (round 6: the rerun took 256 s of the GPU
+   suite's 598, VERDICT r5 item 2);
 2. the `knobs` tests with the product's cap, so every forced order also runs
    its normal ring path (no capped spin allowed).
 The Python paths load the twin through REDSET_HIP_LIBRARY; the C drivers
@@ -61,8 +61,7 @@ TWIN_DIR = os.path.join(ROOT, "redset_amd", "lib_test")
 TWIN = os.path.join(TWIN_DIR, "libredset_hip.so")
 SELF = "tests/test_gpu_test_build.py"
 # the tests whose kernels the twin's ring and claim knobs change
-TWIN_FILES = ("test_gpu_parity.py", "test_gpu_stream.py", "test_gpu_full_digests.py", "test_gpu_hang_contract.py",
-              "test_doc_examples.py", "test_gpu_dist.py", "test_gpu_rebuild_tool.py")
+TWIN_FILES = ("test_gpu_parity.py", "test_gpu_stream.py", "test_gpu_full_digests.py", "test_gpu_hang_contract.py")
 
 
 def _child(tmp_path, name, extra_env, args, timeout, files=None):

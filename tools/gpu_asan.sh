@@ -15,13 +15,19 @@ B=tests/asan/build
 export ASAN_OPTIONS="verify_asan_link_order=0:detect_leaks=${DETECT_LEAKS:-0}:exitcode=86"
 export LSAN_OPTIONS="suppressions=$PWD/tests/asan/lsan.supp"
 export REDSET_HIP_REBUILD_TOOL=$PWD/$B/redset_hip_rebuild RANK_TEST_BIN=$PWD/$B/rank_test SHARDED_TEST_BIN=$PWD/$B/sharded_test
-timeout -k 10 600 python -u -m pytest -x -v --timeout 100 --timeout-method thread \
+# ASAN_KEEP_GOING=1: no -x, so one test's failure does not hide the rest
+# (round 6: a CHECK of ASan's device allocator at process exit, inside the
+# HIP runtime's own teardown, failed one sharded-mpi run once)
+X=-x; [ -n "$ASAN_KEEP_GOING" ] && X=
+timeout -k 10 900 python -u -m pytest $X -v --timeout 100 --timeout-method thread \
   tests/test_gpu_rebuild_tool.py tests/test_gpu_mpi.py "tests/test_gpu_rccl_stub.py::test_sharded_rccl_transport_with_hip_kernels" \
   "tests/test_gpu_rccl_stub.py::test_sharded_reduce_shape_over_mpi" "tests/test_gpu_rccl_stub.py::test_rank_backends_forced_rccl" \
   > "$OUT/asan_tests.log" 2>&1
 s=$?
 tail -5 "$OUT/asan_tests.log"
-grep -c "AddressSanitizer\|LeakSanitizer" "$OUT/asan_tests.log" || true
+echo "ASan reports (real errors): $(grep -c "ERROR: AddressSanitizer\|ERROR: LeakSanitizer" "$OUT/asan_tests.log")"
+echo "ASan runtime CHECK failures at exit: $(grep -c "CHECK failed: sanitizer_allocator_device" "$OUT/asan_tests.log")"
+[ -n "$ASAN_ONLY" ] && exit $s
 [ $s -eq 0 ] || exit $s
 # ThreadSanitizer (make -C tests/asan SANITIZER=thread B=build_tsan): the
 # offline tool's streaming pipeline -- reader, writer, I/O pool and feeder

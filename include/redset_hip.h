@@ -453,7 +453,9 @@ int redset_hip_sharded_get_shape(const redset_hip_sharded* plan, redset_hip_shar
  * compute (compute == NULL at plan time) the sets are pipelined: every set's
  * gather and return is an exchange of its own on a second stream the plan
  * owns, so set k+1's gather (and the first returns) overlap set k's gf_mac on
- * `stream`. With a compute callback the phases run one after another. */
+ * `stream`; in the partial-sum shape set k's exchange overlaps set k+1's
+ * combines and set k's accumulate follows its exchange. With a compute (or
+ * combine) callback the phases run one after another. */
 int redset_hip_sharded_execute(redset_hip_sharded* plan, void* stream);
 /* One phase (REDSET_HIP_PHASE_*), so callers can time them apart; the four in
  * order are one execute. */

@@ -443,6 +443,10 @@ typedef struct {
   unsigned long long scratch_bytes_needed;  /* REDUCE: this process's partial-sum rows */
   unsigned long long scratch_bytes;         /* the gathered slabs */
   int reduce_messages, reduce_recv_messages; /* REDUCE: peer messages per execute, after merging */
+  int reduce_fused;                         /* REDUCE: a host folds its own inputs in with the
+                                               partials it makes (its inputs read once; needs
+                                               more scratch), else it combines them again after
+                                               the exchange */
 } redset_hip_sharded_shape_info;
 /* Copies min(size, sizeof) bytes: callers built against an older header get
  * the fields they know, never a write past their struct. */

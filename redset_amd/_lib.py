@@ -186,6 +186,7 @@ class ShapeInfo(ctypes.Structure):
         ("scratch_bytes", c_ulonglong),
         ("reduce_messages", c_int),
         ("reduce_recv_messages", c_int),
+        ("reduce_fused", c_int),
     ]
 
     def as_dict(self):

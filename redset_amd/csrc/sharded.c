@@ -493,6 +493,10 @@ typedef struct {
   unsigned long long *sent, *recvd; /* [world] rows sent / received */
   long rows;                /* scratch rows per process (the gathered slabs) */
   int ok;                   /* fits, and every output has a contributor */
+  int fused;                /* 1: an output's host folds its own inputs in with the partials it
+                               makes (COMPUTE), and receives every partial into scratch; 0: the
+                               first remote partial lands in the output and the host's own
+                               inputs are combined again in ACCUMULATE (less scratch) */
 } reduce_alloc;
 
 static void ra_free(reduce_alloc* A) {
@@ -612,23 +616,44 @@ static int ra_build(reduce_alloc* A, const redset_hip_rs* rs, int p, int e, int 
             }
         }
   /* receiver h's scratch rows (after its sent ones), in the order (set,
-   * sender, slice, output); the first remote contributor's go straight in
-   * the output */
+   * sender, slice, output). The first remote contributor's row goes
+   * straight into the output when the output's host has no share of its
+   * own to write there first (fused), or always (direct); the fused
+   * allocation is tried first, the direct one if that does not fit */
   A->rows = (long) world * A->mh * (A->d + A->e);
   for (int g = 0; g < world; ++g)
     if (A->S[g] > A->rows || A->S[g] > INT_MAX / 2) A->ok = 0;
-  for (int k = 0; k < A->nsets && A->ok; ++k)
-    for (int h = 0; h < world; ++h)
-      for (int g = 0; g < world; ++g)
-        for (int q = 0; q < A->nslices; ++q)
-          for (int i = ra_lo(A, k, h); i < ra_lo(A, k, h + 1); ++i) {
-            const int o = A->byhost[(size_t) k * A->nout + i];
-            const uint64_t rem = ra_remote(A, k, o);
-            if (!(rem >> g & 1) || (rem & (~rem + 1)) == ((uint64_t) 1 << g)) continue;
-            A->rrow[ra_key(A, k, o, q, g)] = (int) (A->S[h] + A->R[h]++);
-          }
-  for (int g = 0; g < world; ++g)
-    if (A->S[g] + A->R[g] > A->rows) A->ok = 0;
+  int first = 1;
+#if REDSET_HIP_TEST_KNOBS
+  /* test builds: the direct allocation even where the fused one fits, so
+   * small test sets run it (tests/test_mpi_sharded.py) */
+  if (getenv("REDSET_HIP_TEST_REDUCE_DIRECT")) first = 0;
+#endif
+  for (int fused = first; fused >= 0 && A->ok; --fused) {
+    int fits = 1;
+    for (int h = 0; h < world; ++h) A->R[h] = 0;
+    for (int k = 0; k < A->nsets; ++k)
+      for (int h = 0; h < world; ++h)
+        for (int g = 0; g < world; ++g)
+          for (int q = 0; q < A->nslices; ++q)
+            for (int i = ra_lo(A, k, h); i < ra_lo(A, k, h + 1); ++i) {
+              const int o = A->byhost[(size_t) k * A->nout + i];
+              const uint64_t rem = ra_remote(A, k, o);
+              const int own = (int) (A->mask[(size_t) k * A->nout + o] >> h & 1);
+              const size_t key = ra_key(A, k, o, q, g);
+              A->rrow[key] = -1;
+              if (!(rem >> g & 1)) continue;
+              if ((rem & (~rem + 1)) == ((uint64_t) 1 << g) && !(fused && own)) continue; /* direct */
+              A->rrow[key] = (int) (A->S[h] + A->R[h]++);
+            }
+    for (int g = 0; g < world; ++g)
+      if (A->S[g] + A->R[g] > A->rows) fits = 0;
+    if (fits) {
+      A->fused = fused;
+      return 0;
+    }
+  }
+  A->ok = 0;
   return 0;
 }
 
@@ -707,6 +732,13 @@ static int ra_messages(const reduce_alloc* A, const redset_hip_shard_layout* L, 
   return 0;
 }
 
+/* does some partial of output o, slice q, land in its host's scratch? */
+static int ra_has_scratch(const reduce_alloc* A, int k, int o, int q) {
+  for (int g = 0; g < A->world; ++g)
+    if (A->rrow[ra_key(A, k, o, q, g)] >= 0) return 1;
+  return 0;
+}
+
 /* my combines and exchanges of the partial-sum shape (A->ok) */
 static int plan_reduce(redset_hip_sharded* P, const reduce_alloc* A, const redset_hip_shard_layout* L, int kind,
                        int me) {
@@ -728,21 +760,32 @@ static int plan_reduce(redset_hip_sharded* P, const reduce_alloc* A, const redse
     for (int c = 0; c < p && !rc; ++c)
       for (int q = 0; q < A->nslices && !rc; ++q) {
         const size_t n = A->C - (size_t) q * A->W < A->W ? A->C - (size_t) q * A->W : A->W;
-        for (int h = 0; h < world && !rc; ++h)
+        /* the jobs: (h, grp) = (host, 0) the partials for that host (h ==
+         * me: the outputs only my inputs feed); (me, 1) my outputs that
+         * partials arrive for (ACCUMULATE). Fused: (-1, 0) one job making
+         * every output my inputs feed -- partials for other hosts and my own
+         * outputs' shares -- so my inputs are read once, and (me, 1) XORs
+         * the partials in my scratch into my outputs */
+        for (int h = A->fused ? -1 : 0; h < world && !rc; ++h)
           for (int grp = 0; grp < (h == me ? 2 : 1) && !rc; ++grp) {
-            /* grp 0: partials for h (or, h == me, outputs only my inputs
-             * feed: COMPUTE); grp 1: my outputs partials arrive for
-             * (ACCUMULATE) */
+            if (A->fused && h >= 0 && !(h == me && grp == 1)) continue;
             int ns = 0;
             for (int o = 0; o < nout; ++o) {
-              if (A->oc[o].c != c || ra_host(A, k, o) != h) continue;
+              if (A->oc[o].c != c || (h >= 0 && ra_host(A, k, o) != h)) continue;
               const uint64_t rem = ra_remote(A, k, o);
-              if (h != me ? (rem >> me & 1) : (grp == 0 ? rem == 0 : rem != 0)) sel[ns++] = o;
+              const int own = (int) (A->mask[(size_t) k * A->nout + o] >> me & 1);
+              int take;
+              if (h < 0) take = own;  /* fused COMPUTE */
+              else if (h != me) take = (int) (rem >> me & 1);
+              else if (A->fused) take = ra_has_scratch(A, k, o, q);
+              else take = grp == 0 ? rem == 0 : rem != 0;
+              if (take) sel[ns++] = o;
             }
             if (ns == 0) continue;
-            /* my inputs with a coefficient for one of them */
+            /* my inputs with a coefficient for one of them (fused
+             * accumulate: none, the partials only) */
             int ni = 0;
-            for (int t = 0; t < p; ++t) {
+            for (int t = 0; t < p && !(A->fused && grp == 1); ++t) {
               if (A->host[(size_t) k * p + t] != me) continue;
               int used = 0;
               for (int a = 0; a < ns && !used; ++a) used = A->coef[(size_t) sel[a] * p + t] != 0;
@@ -759,14 +802,15 @@ static int plan_reduce(redset_hip_sharded* P, const reduce_alloc* A, const redse
               }
             if (nin == 0) {
               if (grp == 0 && h == me) rc = sfail("sharded plan: an output with no input");
-              continue; /* grp 1: the one partial that arrived is the output */
+              continue; /* grp 1 (direct): the one partial that arrived is the output */
             }
             memset(cf, 0, (size_t) nin * (size_t) ns);
             int ex = extra0;
             for (int a = 0; a < ns; ++a) {
               const int o = sel[a];
               for (int b = 0; b < ni; ++b) cf[(size_t) a * nin + b] = A->coef[(size_t) o * p + ins[b]];
-              op[a] = h == me ? ra_ptr(L, ra_output(A, k, o, q)) : ra_ptr(L, ra_scratch(A, A->srow[ra_key(A, k, o, q, me)]));
+              op[a] = ra_host(A, k, o) == me ? ra_ptr(L, ra_output(A, k, o, q))
+                                             : ra_ptr(L, ra_scratch(A, A->srow[ra_key(A, k, o, q, me)]));
               for (int g = 0; grp == 1 && g < world; ++g)
                 if (ra_remote(A, k, o) >> g & 1 && A->rrow[ra_key(A, k, o, q, g)] >= 0) cf[(size_t) a * nin + ex++] = 1;
             }
@@ -966,6 +1010,7 @@ static int plan_sets(const redset_hip_rs* rs, int p, int e, int kind, int missin
       S->reduce_bytes_sent = A.sent[me] * W;
       S->reduce_bytes_recv = A.recvd[me] * W;
       S->scratch_bytes_needed = (unsigned long long) (A.S[me] + A.R[me]) * W;
+      S->reduce_fused = A.fused;
     }
     if (!rc && want->shape == REDSET_HIP_SHAPE_REDUCE && !A.ok)
       rc = sfail(world < 2 ? "sharded plan: the partial-sum shape needs at least 2 processes"

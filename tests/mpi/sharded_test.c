@@ -293,10 +293,10 @@ int main(int argc, char** argv) {
     redset_hip_sharded_shape_info si;
     if (!pl || redset_hip_sharded_get_shape(pl, &si, sizeof(si)) != 0) continue;
     printf("rank %d: %s shape %s (asked %s): gather busiest %llu B, reduce busiest %llu B (possible %d), "
-           "sent %llu / %llu B, scratch %llu of %llu B\n",
+           "sent %llu / %llu B, scratch %llu of %llu B, fused %d\n",
            me, i == 0 ? "encode" : "rebuild", shape_name(si.shape), shape_name(opts.shape), si.gather_busiest_bytes,
            si.reduce_busiest_bytes, si.reduce_possible, si.gather_bytes_sent, si.reduce_bytes_sent,
-           si.scratch_bytes_needed, si.scratch_bytes);
+           si.scratch_bytes_needed, si.scratch_bytes, si.reduce_fused);
     /* the shape counts (computed from the placement) against the planned
      * lists' own totals */
     redset_hip_sharded_info inf;

@@ -75,22 +75,30 @@ def test_sharded_rccl_transport_with_hip_kernels(shape, np_, p, e, chunk, lost):
     assert _no_leftover_shm()
 
 
+@pytest.mark.parametrize("alloc", ["fused", "direct"])
 @pytest.mark.parametrize("mode", ["--gpu", "--gpu-host"])
 @pytest.mark.parametrize("np_,p,e,chunk,lost,scheme", [(2, 11, 3, 300_001, [1, 2], "rs"), (3, 6, 2, 40_000, [0, 4], "rs"),
                                                         (3, 8, 1, 65536, [3], "xor")])
-def test_sharded_reduce_shape_over_mpi(mode, np_, p, e, chunk, lost, scheme):
+def test_sharded_reduce_shape_over_mpi(alloc, mode, np_, p, e, chunk, lost, scheme):
     """The partial-sum shape with the HIP combine plans (redset_hip_plan_combine)
     over the MPI transport: slabs in HBM (staged through pinned memory) or in
-    page-locked host memory that the combines read and write in place."""
+    page-locked host memory that the combines read and write in place; both
+    row allocations (fused: the product's choice where it fits; direct:
+    forced through the test twin's REDSET_HIP_TEST_REDUCE_DIRECT)."""
     _need()
     cmd = [MPIRUN, "-np", str(np_), "-host", "localhost", DRIVER, mode, str(p), str(e), str(chunk)] + \
         [str(x) for x in lost]
     env = {**os.environ, "SHARDED_TEST_SHAPE": "reduce"}
+    if alloc == "direct":
+        ld = os.environ.get("LD_LIBRARY_PATH")
+        env["LD_LIBRARY_PATH"] = os.path.dirname(TWIN) + (":" + ld if ld else "")
+        env["REDSET_HIP_TEST_REDUCE_DIRECT"] = "1"
     if scheme == "xor":
         env["SHARDED_TEST_SCHEME"] = "xor"
     res = run_group(cmd, 120, env=env)
     assert res.returncode == 0, res.stdout + res.stderr
     assert res.stdout.count("rebuild shape reduce") == np_, res.stdout
+    assert f"fused {int(alloc == 'fused')}" in res.stdout, res.stdout
 
 
 def test_sharded_rccl_transport_xor():

@@ -384,3 +384,37 @@ def test_hip_plan_paths_on_cpu(oracle, transport, shape, mode, scheme, np_, p, e
     assert res.stdout.count("rebuild gather") == np_
     if shape != "auto":
         assert res.stdout.count(f"rebuild shape {shape}") == np_, res.stdout
+
+
+TWIN_DIR = os.path.join(ROOT, "redset_amd", "lib_test")
+
+
+@pytest.mark.parametrize("direct", [0, 1])
+@pytest.mark.parametrize("stand_in", [False, True])
+@pytest.mark.parametrize("scheme,np_,p,e,chunk,lost", [("rs", 2, 11, 3, 30001, [1, 2]), ("rs", 3, 11, 3, 4096, [1, 2]),
+                                                        ("rs", 3, 12, 4, 777, [1, 2, 3]), ("xor", 3, 8, 1, 3001, [3])])
+def test_reduce_shape_both_allocations(oracle, direct, stand_in, scheme, np_, p, e, chunk, lost):
+    """The partial-sum shape's two row allocations (sharded.c ra_build):
+    fused -- an output's host folds its own inputs in with the partials it
+    makes and receives every partial into scratch -- and direct -- the first
+    remote partial lands in the output, the host's own share is combined
+    after the exchange (less scratch). The planner takes fused where it
+    fits; the test twin's REDSET_HIP_TEST_REDUCE_DIRECT forces direct. Both
+    against the oracle, with the oracle's combine callback and (stand_in)
+    with the HIP combine plans on the CPU stand-in."""
+    if not _have() or not os.path.exists(os.path.join(TWIN_DIR, "libredset_hip.so")):
+        pytest.skip("needs MPICH and the test twin")
+    pre = ["-genv", "LD_PRELOAD", HIPSTUB] if stand_in else []
+    cmd = [MPIRUN, "-np", str(np_), "-host", "localhost"] + pre + [DRIVER] + (["--gpu"] if stand_in else []) + \
+        [str(p), str(e), str(chunk)] + [str(x) for x in lost]
+    ld = os.environ.get("LD_LIBRARY_PATH")
+    env = {**os.environ, "SHARDED_TEST_SHAPE": "reduce", "LD_LIBRARY_PATH": TWIN_DIR + (":" + ld if ld else "")}
+    if direct:
+        env["REDSET_HIP_TEST_REDUCE_DIRECT"] = "1"
+    if scheme == "xor":
+        env["SHARDED_TEST_SCHEME"] = "xor"
+    res = run_group(cmd, 120, env=env, cwd="/tmp")
+    assert res.returncode == 0, res.stdout + res.stderr
+    assert res.stdout.count("rebuild gather") == np_
+    assert res.stdout.count(f"rebuild shape reduce") == np_, res.stdout
+    assert f"fused {1 - direct}" in res.stdout, res.stdout

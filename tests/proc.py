@@ -21,6 +21,28 @@ def run_group(cmd, timeout, env=None, cwd=None):
     return subprocess.CompletedProcess(cmd, p.returncode, out, err)
 
 
+def stub_shm():
+    """tests/rcclstub's shared-memory objects (/dev/shm/rcclstub_<pid>_<id>,
+    <pid> = the process that made the unique id)"""
+    return {f for f in os.listdir("/dev/shm") if f.startswith("rcclstub_")}
+
+
+def leaked_stub_shm(before):
+    """objects made since `before` (a stub_shm() snapshot) whose maker has
+    exited or is this process: what a finished run left behind. Another
+    pytest worker's run still in progress (pytest -n) is not counted."""
+    leaked = []
+    for f in sorted(stub_shm() - before):
+        try:
+            pid = int(f.split("_")[1])
+        except (IndexError, ValueError):
+            leaked.append(f)
+            continue
+        if pid == os.getpid() or not os.path.exists(f"/proc/{pid}"):
+            leaked.append(f)
+    return leaked
+
+
 def locked_make(directory, jobs=8, timeout=600):
     """`make -s -C directory` under an exclusive file lock, so parallel test
     workers (pytest -n) that need the same build do not relink it under each

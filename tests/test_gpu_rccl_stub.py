@@ -23,7 +23,7 @@ import tempfile
 import numpy as np
 import pytest
 
-from proc import run_group
+from proc import leaked_stub_shm, run_group, stub_shm
 from test_gpu_mpi import MPIRUN, _have, _logical, _manifests, _mpirun, _setup
 
 pytestmark = pytest.mark.gpu
@@ -43,8 +43,18 @@ def _stub_env(extra=None):
     return env
 
 
+_before = set()
+
+
+@pytest.fixture(autouse=True)
+def _shm_snapshot():
+    global _before
+    _before = stub_shm()
+    yield
+
+
 def _no_leftover_shm():
-    return not [f for f in os.listdir("/dev/shm") if f.startswith("rcclstub_")]
+    return not leaked_stub_shm(_before)
 
 
 def _need():

@@ -10,7 +10,7 @@ import subprocess
 
 import pytest
 
-from proc import run_group
+from proc import leaked_stub_shm, run_group, stub_shm
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 DRIVER = os.path.join(ROOT, "tests", "mpi", "build", "sharded_test")
@@ -347,12 +347,13 @@ def test_rccl_transport_at_world_above_one_on_cpu(oracle, shape, scheme, np_, p,
            "LD_LIBRARY_PATH": RCCLSTUB_DIR + (":" + ld if ld else "")}
     if scheme == "xor":
         env["SHARDED_TEST_SCHEME"] = "xor"
+    before = stub_shm()
     res = run_group(cmd, 120, env=env, cwd="/tmp")
     if res.returncode != 0 and shape == "reduce" and "do not fit" in res.stderr:
         pytest.skip("the partial sums do not fit this placement's scratch")
     assert res.returncode == 0, res.stdout + res.stderr
     assert res.stdout.count("rebuild gather") == np_
-    assert not [f for f in os.listdir("/dev/shm") if f.startswith("rcclstub_")], "stand-in left shared memory"
+    assert not leaked_stub_shm(before), "stand-in left shared memory"
 
 
 @pytest.mark.parametrize("transport", ["mpi", "rccl"])
